@@ -1,0 +1,41 @@
+# Build recipe for the MI355X FEC engine.
+#   make            -> quic_amd/libquic_fec.so (gfx950) + oracle (and oracle/_ref when
+#                      /root/reference is present)
+#   make lib        -> the product library only
+# hipcc cross-compiles gfx950 code objects without a GPU.
+
+ROOT    := $(dir $(abspath $(lastword $(MAKEFILE_LIST))))
+CSRC    := $(ROOT)quic_amd/csrc
+LIB     := $(ROOT)quic_amd/libquic_fec.so
+TABLES  := $(ROOT)quic_amd/data/cauchy_256_tables.bin
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
+            -DQFEC_BUILD -DQFEC_TABLES_PATH='"$(TABLES)"' -Wall -Wno-unused-function
+
+SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/fec_api.cpp
+HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(ROOT)include/quic_fec.h
+OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/fec_api.o
+
+.PHONY: all lib oracle clean
+all: lib oracle
+
+lib: $(LIB)
+
+$(ROOT)build/fec_kernels.o: $(CSRC)/fec_kernels.hip $(HDRS)
+	@mkdir -p $(ROOT)build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(ROOT)build/fec_api.o: $(CSRC)/fec_api.cpp $(HDRS) $(TABLES)
+	@mkdir -p $(ROOT)build
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -s -C $(ROOT)oracle
+
+clean:
+	rm -rf $(ROOT)build $(LIB)
+	$(MAKE) -s -C $(ROOT)oracle clean

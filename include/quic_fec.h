@@ -1,0 +1,117 @@
+/*
+ * quic_fec.h — C ABI of the MI355X-native FEC engine (libquic_fec.so).
+ *
+ * Drop-in boundary for the QuicR packet-group FEC path.  The reference calls the
+ * Longhair codec through three extern "C" entry points
+ * (/root/reference/net/quic/core/libcat/cauchy_256.h:47,78,103); this library exports
+ * the same three symbols with identical semantics, executed by hand-written gfx950
+ * kernels, plus batched device-pointer and host-pointer entry points that process
+ * thousands of independent groups per launch.  Plain pointers and sizes only.
+ *
+ * Return codes (all entry points): 0 = OK; -1 = unsupported parameters, exactly where
+ * the reference returns -1 (m > 1 and (k + m > 256 or block_bytes % 8 != 0));
+ * <= -2 = errors the reference has no code for (bad arguments, GPU runtime failure;
+ * see qfec_last_error()).
+ */
+#ifndef QUIC_AMD_QUIC_FEC_H
+#define QUIC_AMD_QUIC_FEC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CAUCHY_256_VERSION 2
+
+#if defined(QFEC_BUILD)
+#define QFEC_API __attribute__((visibility("default")))
+#else
+#define QFEC_API
+#endif
+
+/* Same layout as cauchy_256.h:52-55. */
+typedef struct _Block {
+    unsigned char *data;
+    unsigned char row;
+} Block;
+
+/* ---------------------------------------------------------------------------------
+ * Single-group drop-ins (host pointers; synchronous).
+ * ------------------------------------------------------------------------------- */
+
+/* Replaces _cauchy_256_init (cauchy_256.h:47, cauchy_256.cpp:389-398).  Returns 0 on
+ * success and -1 on a version mismatch — what the reference code does (its header
+ * comment says otherwise).  Also brings up the default GPU context. */
+QFEC_API int _cauchy_256_init(int expected_version);
+#ifndef cauchy_256_init
+#define cauchy_256_init() _cauchy_256_init(CAUCHY_256_VERSION)
+#endif
+
+/* Replaces cauchy_256_encode (cauchy_256.h:78, cauchy_256.cpp:1502-1601): k data blocks
+ * (pointer array) -> m recovery blocks stored end to end.  k <= 1 copies data[0] into
+ * every output.  For m > 1 with k + m > 256 or block_bytes % 8 != 0 it writes the XOR
+ * parity into the first recovery block and returns -1, like the reference. */
+QFEC_API int cauchy_256_encode(int k, int m, const unsigned char *data_ptrs[], void *recovery_blocks,
+                      int block_bytes);
+
+/* Replaces cauchy_256_decode (cauchy_256.h:103, cauchy_256.cpp:1254-1413): in place.  The
+ * i-th block (array order) tagged row >= k receives the i-th smallest missing data row:
+ * its data is overwritten with that row's data and its row field rewritten. */
+QFEC_API int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes);
+
+/* ---------------------------------------------------------------------------------
+ * Batched engine.  Layouts (row-major, bb = block_bytes):
+ *   data   [G][k][bb]   parity [G][m][bb]
+ *   blocks [G][k][bb]   rows   [G][k]  (u8 row tags, data 0..k-1, parity k..k+m-1)
+ *   status [G]          per-group return code of the equivalent cauchy_256_decode call
+ * `stream` is a hipStream_t (NULL = the context's stream).  Device entry points only
+ * enqueue work; they do not synchronise.
+ * ------------------------------------------------------------------------------- */
+typedef struct qfec_ctx qfec_ctx;
+
+QFEC_API int qfec_ctx_create(int device, qfec_ctx **out);
+QFEC_API void qfec_ctx_destroy(qfec_ctx *ctx);
+/* Pre-size every per-(k, m) table and workspace for up to `groups` groups so that later
+ * calls allocate nothing (required before capturing calls into a HIP graph). */
+QFEC_API int qfec_reserve(qfec_ctx *ctx, int k, int m, int block_bytes, long long groups);
+
+QFEC_API int qfec_encode_batch(qfec_ctx *ctx, int k, int m, int block_bytes, long long groups,
+                      const unsigned char *d_data, unsigned char *d_parity, void *stream);
+
+/* d_out may equal d_blocks (in place, the reference semantics) or be a separate
+ * [G][k][bb] buffer that receives only the recovered blocks.  d_rows_out may equal
+ * d_rows_in.  d_status may be NULL. */
+QFEC_API int qfec_decode_batch(qfec_ctx *ctx, int k, int m, int block_bytes, long long groups,
+                      const unsigned char *d_blocks, const unsigned char *d_rows_in,
+                      unsigned char *d_out, unsigned char *d_rows_out, int *d_status,
+                      void *stream);
+
+/* Host-pointer variants: pinned staging, H2D, kernels, D2H; synchronous.  The decode
+ * works in place on h_blocks / h_rows like cauchy_256_decode. */
+QFEC_API int qfec_encode_batch_host(qfec_ctx *ctx, int k, int m, int block_bytes, long long groups,
+                           const unsigned char *h_data, unsigned char *h_parity);
+QFEC_API int qfec_decode_batch_host(qfec_ctx *ctx, int k, int m, int block_bytes, long long groups,
+                           unsigned char *h_blocks, unsigned char *h_rows, int *h_status);
+
+/* ---------------------------------------------------------------------------------
+ * Support: the coefficient tables, a seeded synthetic workload, diagnostics.
+ * ------------------------------------------------------------------------------- */
+/* Rows 1..m-1 of the Cauchy matrix the reference selects (cauchy_256.cpp:422-480),
+ * (m-1) x k bytes, row-major.  Host only.  Returns -1 if m < 2 or k + m > 256. */
+QFEC_API int qfec_cauchy_matrix(int k, int m, unsigned char *out);
+
+/* Fill d_dst with bytes [byte_offset, byte_offset + bytes) of the splitmix64 stream
+ * (byte_offset % 8 == 0); see quic_amd/synth.py for the definition. */
+QFEC_API int qfec_synth_fill(void *d_dst, unsigned long long bytes, unsigned long long seed,
+                    unsigned long long byte_offset, void *stream);
+/* blocks[g][i] = (src[g][i] < k ? data[g][src] : parity[g][src - k]); src is int16 [G][k]. */
+QFEC_API int qfec_synth_gather(const unsigned char *d_data, const unsigned char *d_parity,
+                      const short *d_src, unsigned char *d_blocks, int k, int m,
+                      int block_bytes, long long groups, void *stream);
+
+QFEC_API const char *qfec_last_error(void);
+QFEC_API int qfec_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QUIC_AMD_QUIC_FEC_H */

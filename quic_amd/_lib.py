@@ -1,0 +1,79 @@
+"""Loader for libquic_fec.so (the HIP extension).  Fails loudly when it is missing.
+
+The product path has no CPU fallback: if the shared library was not built (run
+`make lib` or `python -c "import __graft_entry__ as g; g.build()"`), importing the
+engine raises instead of silently computing on the host.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libquic_fec.so")
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class Block(ctypes.Structure):
+    """cauchy_256.h:52-55 `Block { unsigned char *data; unsigned char row; }`."""
+    _fields_ = [("data", _u8p), ("row", ctypes.c_uint8)]
+
+
+# name -> (restype, argtypes); every symbol include/quic_fec.h declares
+SIGNATURES = {
+    "_cauchy_256_init": (ctypes.c_int, [ctypes.c_int]),
+    "cauchy_256_encode": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_u8p),
+                                         ctypes.c_void_p, ctypes.c_int]),
+    "cauchy_256_decode": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(Block),
+                                         ctypes.c_int]),
+    "qfec_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "qfec_ctx_destroy": (None, [ctypes.c_void_p]),
+    "qfec_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_longlong]),
+    "qfec_encode_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p]),
+    "qfec_decode_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p]),
+    "qfec_encode_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,
+                                              ctypes.c_void_p]),
+    "qfec_decode_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p]),
+    "qfec_cauchy_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    "qfec_synth_fill": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_ulonglong, ctypes.c_ulonglong,
+                                       ctypes.c_ulonglong, ctypes.c_void_p]),
+    "qfec_synth_gather": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p]),
+    "qfec_last_error": (ctypes.c_char_p, []),
+    "qfec_version": (ctypes.c_int, []),
+}
+
+_lib = None
+
+
+def load():
+    """Load libquic_fec.so (cached).  Raises if it is absent or lacks a symbol."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `make lib` (HIP extension required; "
+                          "there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)   # AttributeError if the export is missing
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+class FecError(RuntimeError):
+    def __init__(self, rc, what):
+        msg = load().qfec_last_error()
+        super().__init__(f"{what} failed: rc={rc} ({msg.decode() if msg else ''})")
+        self.rc = rc

@@ -1,0 +1,521 @@
+// fec_api.cpp — host side of libquic_fec.so: the C ABI in include/quic_fec.h.
+//
+// Owns per-device contexts (stream, coefficient tables, decode workspace, pinned
+// staging) and maps the reference's per-group codec calls (cauchy_256.h) and the batched
+// calls onto the gfx950 kernels in fec_kernels.hip.  There is no CPU compute path: every
+// parity / recovered byte is produced on the GPU; if the device is unusable the calls
+// fail with a negative code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/quic_fec.h"
+#include "fec_kernels.h"
+#include "gf256.h"
+
+// ------------------------------------------------------------- Cauchy table blob
+// quic_amd/data/cauchy_256_tables.bin (tools/gen_cauchy_tables.py) embedded at build time:
+// M2[1*254] | M3[2*253] | M4[3*252] | M5[4*251] | M6[5*250] | Y[256] | X[30876]
+#ifndef QFEC_TABLES_PATH
+#error "QFEC_TABLES_PATH must name quic_amd/data/cauchy_256_tables.bin"
+#endif
+__asm__(".section .rodata\n"
+        ".balign 16\n"
+        ".hidden qfec_cauchy_blob\n"
+        ".globl qfec_cauchy_blob\n"
+        "qfec_cauchy_blob:\n"
+        ".incbin \"" QFEC_TABLES_PATH "\"\n"
+        ".hidden qfec_cauchy_blob_end\n"
+        ".globl qfec_cauchy_blob_end\n"
+        "qfec_cauchy_blob_end:\n"
+        ".previous\n");
+extern "C" const unsigned char qfec_cauchy_blob[];
+extern "C" const unsigned char qfec_cauchy_blob_end[];
+
+namespace {
+
+enum {
+    T_M2 = 0, T_M3 = T_M2 + 254, T_M4 = T_M3 + 506, T_M5 = T_M4 + 756, T_M6 = T_M5 + 1004,
+    T_Y = T_M6 + 1250, T_X = T_Y + 256, T_SIZE = T_X + 30876
+};
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return -100 - (int)e;
+}
+
+#define QF_HIP(expr)                                   \
+    do {                                               \
+        hipError_t _e = (expr);                        \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+bool blob_ok() { return (qfec_cauchy_blob_end - qfec_cauchy_blob) == T_SIZE; }
+
+// cauchy_matrix(), cauchy_256.cpp:422-480: rows y = 1..m-1, (m-1) x k.
+int cauchy_rows(int k, int m, uint8_t* out) {
+    if (m < 2 || k < 1 || k + m > 256) return -1;
+    const uint8_t* tb = qfec_cauchy_blob;
+    if (m <= 6) {
+        static const int base[7] = {0, 0, T_M2, T_M3, T_M4, T_M5, T_M6};
+        const int stride = 256 - m;
+        for (int y = 1; y < m; ++y)
+            for (int x = 0; x < k; ++x) out[(y - 1) * k + x] = tb[base[m] + (y - 1) * stride + x];
+        return 0;
+    }
+    const int n = m - 7;
+    const uint8_t* X = tb + T_X + n * 249 - n * (n + 1) / 2;
+    const uint8_t* Y = tb + T_Y;
+    for (int y = 1; y < m; ++y) {
+        const uint8_t G = Y[y - 1];
+        out[(y - 1) * k] = qfec::gf_inv(1 ^ G);
+        for (int x = 1; x < k; ++x) {
+            const uint8_t B = X[x - 1];
+            out[(y - 1) * k + x] = qfec::gf_div(B, B ^ G);
+        }
+    }
+    return 0;
+}
+
+int pow2_at_least(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+int encode_rc(int m) { return std::min(pow2_at_least(m), 16); }
+int decode_rc(int rmax) { return std::min(pow2_at_least(rmax), 8); }
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= n) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; n = 0; }
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipSuccess) n = bytes;
+        return e;
+    }
+};
+
+struct HostBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    ~HostBuf() { if (p) (void)hipHostFree(p); }
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= n) return hipSuccess;
+        if (p) { (void)hipHostFree(p); p = nullptr; n = 0; }
+        hipError_t e = hipHostMalloc(&p, bytes, 0);
+        if (e == hipSuccess) n = bytes;
+        return e;
+    }
+};
+
+}  // namespace
+
+struct qfec_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // encode coefficient tables keyed by (k, m, rc): [nchunk][k][rcp]; decode cenc by (k, m)
+    std::map<std::tuple<int, int, int>, std::unique_ptr<DevBuf>> enc_tab;
+    std::map<std::pair<int, int>, std::unique_ptr<DevBuf>> cenc_tab;
+    DevBuf dcoef, dslots, dnout, dscratch;
+    HostBuf h_stage;
+    DevBuf d_stage;
+    std::mutex mu;   // one caller at a time per context (the reference is single-threaded)
+};
+
+namespace {
+
+int set_device(qfec_ctx* c) {
+    QF_HIP(hipSetDevice(c->device));
+    return 0;
+}
+
+hipStream_t pick(qfec_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+// Encode coefficient table: output o = chunk*rc + j; o == 0 is the all-ones row.
+int get_enc_table(qfec_ctx* c, int k, int m, int rc, const uint8_t** out) {
+    auto key = std::make_tuple(k, m, rc);
+    auto it = c->enc_tab.find(key);
+    if (it != c->enc_tab.end()) { *out = (const uint8_t*)it->second->p; return 0; }
+    const int rcp = std::max(rc, 4);
+    const int nchunk = (m + rc - 1) / rc;
+    std::vector<uint8_t> C((size_t)std::max(m - 1, 1) * k);
+    if (cauchy_rows(k, m, C.data())) return fail(-1, "no Cauchy matrix for (k, m)");
+    std::vector<uint8_t> tab((size_t)nchunk * k * rcp, 0);
+    for (int o = 0; o < m; ++o) {
+        const int ch = o / rc, j = o % rc;
+        for (int x = 0; x < k; ++x)
+            tab[((size_t)ch * k + x) * rcp + j] = o == 0 ? 1 : C[(size_t)(o - 1) * k + x];
+    }
+    auto buf = std::make_unique<DevBuf>();
+    QF_HIP(buf->ensure(tab.size()));
+    QF_HIP(hipMemcpy(buf->p, tab.data(), tab.size(), hipMemcpyHostToDevice));
+    *out = (const uint8_t*)buf->p;
+    c->enc_tab.emplace(key, std::move(buf));
+    return 0;
+}
+
+int get_cenc(qfec_ctx* c, int k, int m, const uint8_t** out) {
+    auto key = std::make_pair(k, m);
+    auto it = c->cenc_tab.find(key);
+    if (it != c->cenc_tab.end()) { *out = (const uint8_t*)it->second->p; return 0; }
+    std::vector<uint8_t> t((size_t)m * k, 1);
+    if (k + m <= 256 && m >= 2) {
+        if (cauchy_rows(k, m, t.data() + k)) return fail(-1, "no Cauchy matrix for (k, m)");
+    }
+    auto buf = std::make_unique<DevBuf>();
+    QF_HIP(buf->ensure(t.size()));
+    QF_HIP(hipMemcpy(buf->p, t.data(), t.size(), hipMemcpyHostToDevice));
+    *out = (const uint8_t*)buf->p;
+    c->cenc_tab.emplace(key, std::move(buf));
+    return 0;
+}
+
+int decode_workspace(qfec_ctx* c, int k, int rmax, int rc, long long groups) {
+    const int rcp = std::max(rc, 4);
+    const int nchunk = (rmax + rc - 1) / rc;
+    QF_HIP(c->dcoef.ensure((size_t)groups * nchunk * k * rcp));
+    QF_HIP(c->dslots.ensure((size_t)groups * rmax));
+    QF_HIP(c->dnout.ensure((size_t)groups * sizeof(int32_t)));
+    return 0;
+}
+
+int check_common(qfec_ctx* c, int k, int m, int bb, long long groups) {
+    if (!c) return fail(-2, "null context");
+    if (!blob_ok()) return fail(-2, "embedded Cauchy tables have the wrong size");
+    if (k < 1 || m < 1 || bb < 1 || groups < 0) return fail(-2, "bad k / m / block_bytes / groups");
+    if (k > 255) return fail(-2, "k > 255 cannot be tagged by an 8-bit row");
+    return 0;
+}
+
+int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d_data,
+                uint8_t* d_par, hipStream_t st) {
+    if (G == 0) return 0;
+    if (k <= 1) {   // cauchy_256.cpp:1508-1516
+        QF_HIP(qfec::launch_replicate(d_data, d_par, m, bb, G, st));
+        return 0;
+    }
+    // P0 = XOR of the data (:1519-1523).  For m == 1 that is the whole answer; for
+    // m > 1 with unsupported parameters the reference still writes it before
+    // returning -1 (:1532-1534).
+    if (m == 1 || k + m > 256 || bb % 8 != 0) {
+        QF_HIP(qfec::launch_xor_encode(d_data, d_par, k, bb, G, (long long)m * bb, st));
+        return m == 1 ? 0 : fail(-1, "unsupported (k + m > 256 or block_bytes % 8 != 0)");
+    }
+    const int rc = encode_rc(m);
+    const uint8_t* tab = nullptr;
+    int rcode = get_enc_table(c, k, m, rc, &tab);
+    if (rcode) return rcode;
+    QF_HIP(qfec::launch_gf_encode(d_data, d_par, tab, k, m, bb, G, rc, st));
+    return 0;
+}
+
+int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d_blocks,
+                const uint8_t* d_rows_in, uint8_t* d_out, uint8_t* d_rows_out, int32_t* d_status,
+                hipStream_t st) {
+    if (G == 0) return 0;
+    if (k <= 1) {   // cauchy_256.cpp:1257-1261
+        QF_HIP(qfec::launch_rows_k1(d_rows_in, d_rows_out, d_status, G, st));
+        return 0;
+    }
+    if (m == 1) {   // :1264-1267
+        QF_HIP(qfec::launch_xor_decode(d_blocks, d_out, d_rows_in, d_rows_out, d_status, k, bb, G,
+                                       st));
+        return 0;
+    }
+    const int rmax = std::min(k, m);
+    const int rc = decode_rc(rmax);
+    const int nchunk = (rmax + rc - 1) / rc;
+    const uint8_t* cenc = nullptr;
+    int r = get_cenc(c, k, m, &cenc);
+    if (r) return r;
+    if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
+    qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
+    QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc, rmax,
+                                    G, st));
+    if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
+    if (nchunk > 1 && d_out == d_blocks) {
+        // in place with several output chunks: a later chunk would read slots an earlier
+        // chunk already overwrote, so stage the recovered blocks first
+        QF_HIP(c->dscratch.ensure((size_t)G * rmax * bb));
+        QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, (uint8_t*)c->dscratch.p, w, k, m, bb, G,
+                                              rc, rmax, st));
+        QF_HIP(qfec::launch_scatter_recovered((const uint8_t*)c->dscratch.p, d_out, w, k, bb,
+                                              rmax, G, st));
+        return 0;
+    }
+    QF_HIP(qfec::launch_gf_decode(d_blocks, d_out, w, k, m, bb, G, rc, rmax, st));
+    return 0;
+}
+
+// Default context for the single-group drop-ins (created on the caller's current device).
+std::once_flag g_default_once;
+qfec_ctx* g_default = nullptr;
+int g_default_rc = 0;
+
+int default_ctx(qfec_ctx** out) {
+    std::call_once(g_default_once, [] {
+        int dev = 0;
+        if (const char* e = getenv("QFEC_DEVICE")) dev = atoi(e);
+        else if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+        g_default_rc = qfec_ctx_create(dev, &g_default);
+    });
+    *out = g_default;
+    if (!g_default) return g_default_rc ? g_default_rc : fail(-2, "no default GPU context");
+    return 0;
+}
+
+}  // namespace
+
+// ======================================================================== C ABI
+extern "C" {
+
+int qfec_version(void) { return 1; }
+
+const char* qfec_last_error(void) { return g_err.c_str(); }
+
+int qfec_cauchy_matrix(int k, int m, unsigned char* out) {
+    if (!blob_ok()) return fail(-2, "embedded Cauchy tables have the wrong size");
+    return cauchy_rows(k, m, out);
+}
+
+int qfec_ctx_create(int device, qfec_ctx** out) {
+    if (!out) return fail(-2, "null out");
+    *out = nullptr;
+    int n = 0;
+    QF_HIP(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(-2, "no such HIP device");
+    auto c = std::make_unique<qfec_ctx>();
+    c->device = device;
+    QF_HIP(hipSetDevice(device));
+    QF_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    *out = c.release();
+    return 0;
+}
+
+void qfec_ctx_destroy(qfec_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int qfec_encode_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
+                      const unsigned char* d_data, unsigned char* d_parity, void* stream) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    if (groups && (!d_data || !d_parity)) return fail(-2, "null buffer");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    return encode_impl(c, k, m, bb, groups, d_data, d_parity, pick(c, stream));
+}
+
+int qfec_decode_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
+                      const unsigned char* d_blocks, const unsigned char* d_rows_in,
+                      unsigned char* d_out, unsigned char* d_rows_out, int* d_status,
+                      void* stream) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    if (groups && (!d_blocks || !d_rows_in || !d_out || !d_rows_out))
+        return fail(-2, "null buffer");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    return decode_impl(c, k, m, bb, groups, d_blocks, d_rows_in, d_out, d_rows_out,
+                       (int32_t*)d_status, pick(c, stream));
+}
+
+int qfec_encode_batch_host(qfec_ctx* c, int k, int m, int bb, long long groups,
+                           const unsigned char* h_data, unsigned char* h_parity) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    if (groups == 0) return 0;
+    if (!h_data || !h_parity) return fail(-2, "null buffer");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    // chunk the batch so the device staging stays bounded (~1 GiB)
+    const size_t per = (size_t)(k + m) * bb;
+    const long long step = std::max<long long>(1, (long long)((1ull << 30) / per));
+    const long long chunk = std::min(groups, step);
+    QF_HIP(c->d_stage.ensure((size_t)chunk * per));
+    uint8_t* dd = (uint8_t*)c->d_stage.p;
+    uint8_t* dp = dd + (size_t)chunk * k * bb;
+    int result = 0;
+    for (long long g0 = 0; g0 < groups; g0 += chunk) {
+        const long long n = std::min(chunk, groups - g0);
+        QF_HIP(hipMemcpyAsync(dd, h_data + (size_t)g0 * k * bb, (size_t)n * k * bb,
+                              hipMemcpyHostToDevice, c->stream));
+        if (m > 1 && k > 1) QF_HIP(hipMemsetAsync(dp, 0, (size_t)n * m * bb, c->stream));
+        const int r = encode_impl(c, k, m, bb, n, dd, dp, c->stream);
+        if (r < -1) return r;
+        if (r) result = r;
+        QF_HIP(hipMemcpyAsync(h_parity + (size_t)g0 * m * bb, dp, (size_t)n * m * bb,
+                              hipMemcpyDeviceToHost, c->stream));
+    }
+    QF_HIP(hipStreamSynchronize(c->stream));
+    return result;
+}
+
+int qfec_decode_batch_host(qfec_ctx* c, int k, int m, int bb, long long groups,
+                           unsigned char* h_blocks, unsigned char* h_rows, int* h_status) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    if (groups == 0) return 0;
+    if (!h_blocks || !h_rows) return fail(-2, "null buffer");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    const size_t per = (size_t)k * bb + k + sizeof(int32_t);
+    const long long step = std::max<long long>(1, (long long)((1ull << 30) / per));
+    const long long chunk = std::min(groups, step);
+    QF_HIP(c->d_stage.ensure((size_t)chunk * per + 16));
+    uint8_t* db = (uint8_t*)c->d_stage.p;
+    uint8_t* dr = db + (size_t)chunk * k * bb;
+    int32_t* ds = (int32_t*)(((uintptr_t)(dr + (size_t)chunk * k) + 3) & ~(uintptr_t)3);
+    std::vector<int32_t> st_tmp;
+    for (long long g0 = 0; g0 < groups; g0 += chunk) {
+        const long long n = std::min(chunk, groups - g0);
+        QF_HIP(hipMemcpyAsync(db, h_blocks + (size_t)g0 * k * bb, (size_t)n * k * bb,
+                              hipMemcpyHostToDevice, c->stream));
+        QF_HIP(hipMemcpyAsync(dr, h_rows + (size_t)g0 * k, (size_t)n * k, hipMemcpyHostToDevice,
+                              c->stream));
+        const int r = decode_impl(c, k, m, bb, n, db, dr, db, dr, ds, c->stream);
+        if (r) return r;
+        QF_HIP(hipMemcpyAsync(h_blocks + (size_t)g0 * k * bb, db, (size_t)n * k * bb,
+                              hipMemcpyDeviceToHost, c->stream));
+        QF_HIP(hipMemcpyAsync(h_rows + (size_t)g0 * k, dr, (size_t)n * k, hipMemcpyDeviceToHost,
+                              c->stream));
+        if (h_status) {
+            QF_HIP(hipMemcpyAsync(h_status + g0, ds, (size_t)n * sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, c->stream));
+        }
+    }
+    QF_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int qfec_synth_fill(void* d_dst, unsigned long long bytes, unsigned long long seed,
+                    unsigned long long byte_offset, void* stream) {
+    QF_HIP(qfec::launch_synth_fill((uint8_t*)d_dst, bytes, seed, byte_offset,
+                                   (hipStream_t)stream));
+    return 0;
+}
+
+int qfec_synth_gather(const unsigned char* d_data, const unsigned char* d_parity,
+                      const short* d_src, unsigned char* d_blocks, int k, int m, int bb,
+                      long long groups, void* stream) {
+    QF_HIP(qfec::launch_synth_gather(d_data, d_parity, (const int16_t*)d_src, d_blocks, k, m, bb,
+                                     groups, (hipStream_t)stream));
+    return 0;
+}
+
+// ---------------------------------------------------------- single-group drop-ins
+int _cauchy_256_init(int expected_version) {
+    if (expected_version != CAUCHY_256_VERSION) return -1;   // cauchy_256.cpp:389-398
+    qfec_ctx* c;
+    return default_ctx(&c);
+}
+
+int cauchy_256_encode(int k, int m, const unsigned char* data_ptrs[], void* recovery_blocks,
+                      int block_bytes) {
+    qfec_ctx* c;
+    int rc = default_ctx(&c);
+    if (rc) return rc;
+    if ((rc = check_common(c, k, m, block_bytes, 1))) return rc;
+    if (!data_ptrs || !recovery_blocks) return fail(-2, "null buffer");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    const size_t bb = (size_t)block_bytes;
+    const size_t in_bytes = (size_t)k * bb, out_bytes = (size_t)m * bb;
+    QF_HIP(c->h_stage.ensure(in_bytes + out_bytes));
+    QF_HIP(c->d_stage.ensure(in_bytes + out_bytes));
+    uint8_t* hs = (uint8_t*)c->h_stage.p;
+    for (int x = 0; x < k; ++x) memcpy(hs + x * bb, data_ptrs[x], bb);
+    uint8_t* dd = (uint8_t*)c->d_stage.p;
+    QF_HIP(hipMemcpyAsync(dd, hs, in_bytes, hipMemcpyHostToDevice, c->stream));
+    // outputs the reference leaves untouched (the -1 paths) keep the caller's bytes
+    QF_HIP(hipMemcpyAsync(dd + in_bytes, recovery_blocks, out_bytes, hipMemcpyHostToDevice,
+                          c->stream));
+    if (m > 1 && k > 1 && k + m <= 256 && bb % 8 == 0)   // :1554 zeroes rows 1..m-1
+        QF_HIP(hipMemsetAsync(dd + in_bytes, 0, out_bytes, c->stream));
+    rc = encode_impl(c, k, m, block_bytes, 1, dd, dd + in_bytes, c->stream);
+    if (rc < -1) return rc;
+    QF_HIP(hipMemcpyAsync(hs + in_bytes, dd + in_bytes, out_bytes, hipMemcpyDeviceToHost,
+                          c->stream));
+    QF_HIP(hipStreamSynchronize(c->stream));
+    memcpy(recovery_blocks, hs + in_bytes, out_bytes);
+    return rc;
+}
+
+int cauchy_256_decode(int k, int m, Block* blocks, int block_bytes) {
+    qfec_ctx* c;
+    int rc = default_ctx(&c);
+    if (rc) return rc;
+    if ((rc = check_common(c, k, m, block_bytes, 1))) return rc;
+    if (!blocks) return fail(-2, "null buffer");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    const size_t bb = (size_t)block_bytes;
+    const size_t data_bytes = (size_t)k * bb;
+    QF_HIP(c->h_stage.ensure(data_bytes + 256 + 16));
+    QF_HIP(c->d_stage.ensure(data_bytes + 256 + 16));
+    uint8_t* hs = (uint8_t*)c->h_stage.p;
+    uint8_t* hr = hs + data_bytes;
+    int32_t* hst = (int32_t*)(((uintptr_t)(hr + 256) + 3) & ~(uintptr_t)3);
+    for (int x = 0; x < k; ++x) {
+        memcpy(hs + x * bb, blocks[x].data, bb);
+        hr[x] = blocks[x].row;
+    }
+    uint8_t* dd = (uint8_t*)c->d_stage.p;
+    uint8_t* dr = dd + data_bytes;
+    int32_t* dst = (int32_t*)(((uintptr_t)(dr + 256) + 3) & ~(uintptr_t)3);
+    QF_HIP(hipMemcpyAsync(dd, hs, data_bytes + 256, hipMemcpyHostToDevice, c->stream));
+    rc = decode_impl(c, k, m, block_bytes, 1, dd, dr, dd, dr, dst, c->stream);
+    if (rc) return rc;
+    QF_HIP(hipMemcpyAsync(hs, dd, data_bytes + k, hipMemcpyDeviceToHost, c->stream));
+    QF_HIP(hipMemcpyAsync(hst, dst, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    QF_HIP(hipStreamSynchronize(c->stream));
+    for (int x = 0; x < k; ++x) {
+        if (blocks[x].row >= k || hr[x] != blocks[x].row)   // only recovery slots change
+            memcpy(blocks[x].data, hs + x * bb, bb);
+        blocks[x].row = hr[x];
+    }
+    return *hst;
+}
+
+int qfec_reserve(qfec_ctx* c, int k, int m, int bb, long long groups) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    if (m > 1 && k > 1 && k + m <= 256) {
+        const uint8_t* t;
+        if ((rc = get_enc_table(c, k, m, encode_rc(m), &t))) return rc;
+    }
+    if (m > 1 && k > 1) {
+        const uint8_t* t;
+        if ((rc = get_cenc(c, k, m, &t))) return rc;
+        const int rmax = std::min(k, m);
+        if ((rc = decode_workspace(c, k, rmax, decode_rc(rmax), groups))) return rc;
+        if (rmax > decode_rc(rmax)) QF_HIP(c->dscratch.ensure((size_t)groups * rmax * bb));
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// fec_kernels.h — launch interface of the gfx950 FEC kernels (internal to libquic_fec.so).
+//
+// Layouts (all device memory, row-major, bb = block_bytes, s = bb / 8):
+//   data     [G][k][bb]   the k data blocks of each packet group
+//   parity   [G][m][bb]   encode output (parity block y of group g at (g*m + y)*bb)
+//   blocks   [G][k][bb]   decode input: the first k packets received, any order
+//   rows     [G][k]       row tag of each received block (data 0..k-1, parity k..k+m-1)
+// The bit-sliced code treats every block as 8 sub-rows of s bytes; see DESIGN.md.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qfec {
+
+// Decode work tables written by the prep kernel and read by the apply kernel.
+struct DecodeWork {
+    uint8_t* coef;     // [G][nchunk][k][RCP]  bit-sliced GF(256) coefficients
+    uint8_t* slots;    // [G][RMAX]            output slot (0..k-1) of recovered block j
+    int32_t* nout;     // [G]                  number of recovered blocks in this group
+};
+
+// parity[g*out_gstride ..+bb) = XOR of the k blocks of group g (m == 1 encode, and the
+// P0 the reference writes before rejecting invalid m > 1 parameters).
+hipError_t launch_xor_encode(const uint8_t* data, uint8_t* parity, int k, int bb,
+                             long long groups, long long out_gstride, hipStream_t st);
+
+// m == 1 decode: XOR the k-1 other blocks into the block tagged row >= k.
+hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t* rows_in,
+                             uint8_t* rows_out, int32_t* status, int k, int bb,
+                             long long groups, hipStream_t st);
+
+// k <= 1 encode: copy data[0] into each of the m outputs (cauchy_256.cpp:1508-1516).
+hipError_t launch_replicate(const uint8_t* data, uint8_t* parity, int m, int bb,
+                            long long groups, hipStream_t st);
+
+// k <= 1 decode: row := 0 (cauchy_256.cpp:1257-1261).
+hipError_t launch_rows_k1(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
+                          long long groups, hipStream_t st);
+
+// Bit-sliced GF(256) apply.  Encode: coef is the shared [nchunk][k][RCP] table built
+// from the Cauchy matrix (row 0 = ones), outputs are parity rows chunk*RC + j.
+hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t* coef,
+                            int k, int m, int bb, long long groups, int rc, hipStream_t st);
+
+// Decode prep: per group, sort blocks, invert the erasure submatrix in GF(256) and
+// emit the r x k recovery coefficients.  cenc is the [m][k] encode matrix (row 0 = ones).
+hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
+                              const uint8_t* cenc, DecodeWork w, int k, int m, int bb,
+                              int rc, int rmax, long long groups, hipStream_t st);
+
+// Decode apply: recovered block j of group g = sum_pos coef[g][..][pos][j] (x) blocks[g][pos],
+// written to out[g][slots[g][j]].
+hipError_t launch_gf_decode(const uint8_t* blocks, uint8_t* out, DecodeWork w, int k, int m,
+                            int bb, long long groups, int rc, int rmax, hipStream_t st);
+
+// In-place decode when rmax > rc: apply into scratch [G][rmax][bb], then scatter to slots.
+hipError_t launch_gf_decode_scratch(const uint8_t* blocks, uint8_t* scratch, DecodeWork w,
+                                   int k, int m, int bb, long long groups, int rc, int rmax,
+                                   hipStream_t st);
+hipError_t launch_scatter_recovered(const uint8_t* scratch, uint8_t* out, DecodeWork w, int k,
+                                   int bb, int rmax, long long groups, hipStream_t st);
+
+// Synthetic workload helpers (bench / tests): splitmix64 stream and receive-set gather.
+hipError_t launch_synth_fill(uint8_t* dst, unsigned long long bytes, unsigned long long seed,
+                             unsigned long long byte_offset, hipStream_t st);
+hipError_t launch_synth_gather(const uint8_t* data, const uint8_t* parity, const int16_t* src,
+                               uint8_t* blocks, int k, int m, int bb, long long groups,
+                               hipStream_t st);
+
+}  // namespace qfec

@@ -1,0 +1,740 @@
+// fec_kernels.hip — gfx950 kernels for QuicR packet-group FEC (encode + erasure recover).
+//
+// The reference codec (libcat cauchy_256, net/quic/core/libcat/cauchy_256.cpp) is a
+// bit-sliced Cauchy Reed-Solomon code over GF(2^8): each block of bb bytes is 8 sub-rows
+// of s = bb/8 bytes and a GF(256) coefficient c acts on a block through its transposed
+// 8x8 bit expansion
+//      out[r][j] ^= XOR_{t : bit t of (c * alpha^r)} in[t][j]          (j = byte column)
+// i.e. pure byte XORs between sub-rows at the SAME column j.  No multiplications touch
+// the data, so the work is HBM-bound byte streaming (no MFMA: nothing here is a
+// floating-point contraction).
+//
+// Kernel set (all wave64, 256-thread workgroups = 4 independent waves):
+//   xor_encode / xor_decode   m = 1 XOR parity (cauchy_256.cpp:1519-1528, :486-540)
+//   gf_apply<RC>              bit-sliced GF(256) matrix x blocks, RC outputs per wave;
+//                             used for encode (Cauchy rows, :1502-1601) and for decode
+//                             (per-group recovery rows from the prep kernel)
+//   decode_prep               per-group GF(256) inverse of the erasure submatrix
+//                             (replaces sort_blocks/eliminate_original/bitmatrix GE,
+//                             :543-1252: same unique solution, one pass over the data)
+//
+// The coefficient of a (output, input) pair is wave-uniform, so it lives in SGPRs and the
+// 8x8 expansion is a scalar branch over its two nibbles; the data lane only ever runs
+// v_xor / v_bitop3 (3-input XOR).  See DESIGN.md "Kernels" for the derivation of the
+// W/Z recurrences used below.
+#include "fec_kernels.h"
+#include "gf256.h"
+
+namespace qfec {
+
+typedef uint32_t u32ua __attribute__((aligned(1)));   // unaligned dword (gfx950 unaligned mode)
+typedef uint64_t u64a __attribute__((aligned(8)));
+typedef uint32_t u32x4a16 __attribute__((ext_vector_type(4), aligned(16)));
+typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
+
+__constant__ GfTables c_gf = make_gf_tables();
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // v_bitop3_b32 ... bitop3:0x96
+}
+
+__device__ __forceinline__ int wave_id() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+// ------------------------------------------------------------------ m = 1 XOR paths
+// Vector access policy: V is the per-lane access type.  Tail bytes (bb % sizeof(V)) are
+// handled bytewise by the first lanes.
+// Variant index -> access type: 0 16B (16-aligned), 1 16B (8-aligned), 2 8B, 3 4B, 4 1B.
+template <int VAR> struct Vec;
+template <> struct Vec<0> { typedef u32x4a16 T; static constexpr int N = 16; };
+template <> struct Vec<1> { typedef u32x4a8 T;  static constexpr int N = 16; };
+template <> struct Vec<2> { typedef uint64_t T; static constexpr int N = 8; };
+template <> struct Vec<3> { typedef uint32_t T; static constexpr int N = 4; };
+template <> struct Vec<4> { typedef uint8_t T;  static constexpr int N = 1; };
+
+// parity[g] = XOR_x data[g][x]; one wave per group.
+template <int VAR, int K>
+__global__ __launch_bounds__(256) void xor_encode_kernel(const uint8_t* __restrict__ data,
+                                                         uint8_t* __restrict__ parity, int k,
+                                                         int bb, long long groups,
+                                                         long long ostride) {
+    const int lane = threadIdx.x & 63;
+    const long long g = (long long)blockIdx.x * 4 + wave_id();
+    if (g >= groups) return;
+    typedef typename Vec<VAR>::T V;
+    const int kk = K ? K : k;
+    constexpr int VS = Vec<VAR>::N;
+    const int nq = bb / VS;
+    const uint8_t* src = data + g * (long long)kk * bb;
+    uint8_t* dst = parity + g * ostride;
+    for (int q = lane; q < nq; q += 64) {
+        const uint8_t* p = src + q * VS;
+        V acc = *(const V*)p;
+        if (K) {
+#pragma unroll
+            for (int x = 1; x < (K ? K : 1); ++x) acc ^= *(const V*)(p + (long long)x * bb);
+        } else {
+            for (int x = 1; x < kk; ++x) acc ^= *(const V*)(p + (long long)x * bb);
+        }
+        *(V*)(dst + q * VS) = acc;
+    }
+    for (int i = nq * VS + lane; i < bb; i += 64) {   // tail bytes
+        uint8_t acc = src[i];
+        for (int x = 1; x < kk; ++x) acc ^= src[(long long)x * bb + i];
+        dst[i] = acc;
+    }
+}
+
+// m = 1 decode (cauchy_decode_m1, cauchy_256.cpp:486-540): the first slot with row >= k is
+// the erased slot e; out[e] = XOR of all k slots (its own parity included); its row becomes
+// the first data row not tagged by another slot.  One wave per group.
+template <int VAR>
+__global__ __launch_bounds__(256) void xor_decode_kernel(
+    const uint8_t* __restrict__ blocks, uint8_t* out, const uint8_t* __restrict__ rows_in,
+    uint8_t* rows_out, int32_t* __restrict__ status, int k, int bb, long long groups) {
+    __shared__ uint8_t seen[4][256];
+    const int lane = threadIdx.x & 63;
+    const int w = wave_id();
+    const long long g = (long long)blockIdx.x * 4 + w;
+    if (g >= groups) return;
+    const uint8_t* rg = rows_in + g * k;
+    uint8_t* sw = seen[w];
+    for (int i = lane; i < 256; i += 64) sw[i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    int e = -1;
+    for (int base = 0; base < k && e < 0; base += 64) {
+        const int i = base + lane;
+        const bool er = i < k && rg[i] >= k;
+        const unsigned long long msk = __ballot(er);
+        if (msk) e = base + __ffsll((long long)msk) - 1;
+    }
+    e = __builtin_amdgcn_readfirstlane(e);
+    if (status && lane == 0) status[g] = 0;
+    uint8_t* ro = rows_out + g * k;
+    if (ro != rg)
+        for (int i = lane; i < k; i += 64) ro[i] = rg[i];
+    if (e < 0) return;   // nothing erased
+    for (int i = lane; i < k; i += 64)
+        if (i != e && rg[i] < k) sw[rg[i]] = 1;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    int miss = -1;
+    for (int base = 0; base < k && miss < 0; base += 64) {
+        const int x = base + lane;
+        const unsigned long long msk = __ballot(x < k && !sw[x]);
+        if (msk) miss = base + __ffsll((long long)msk) - 1;
+    }
+    const uint8_t* src = blocks + g * (long long)k * bb;
+    uint8_t* dst = out + g * (long long)k * bb + (long long)e * bb;
+    typedef typename Vec<VAR>::T V;
+    constexpr int VS = Vec<VAR>::N;
+    const int nq = bb / VS;
+    for (int q = lane; q < nq; q += 64) {
+        const uint8_t* p = src + q * VS;
+        V acc = *(const V*)(p + (long long)e * bb);
+        for (int x = 0; x < k; ++x)
+            if (x != e) acc ^= *(const V*)(p + (long long)x * bb);
+        *(V*)(dst + q * VS) = acc;
+    }
+    for (int i = nq * VS + lane; i < bb; i += 64) {
+        uint8_t acc = src[(long long)e * bb + i];
+        for (int x = 0; x < k; ++x)
+            if (x != e) acc ^= src[(long long)x * bb + i];
+        dst[i] = acc;
+    }
+    if (lane == 0 && miss >= 0) ro[e] = (uint8_t)miss;
+}
+
+__global__ void replicate_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ parity,
+                                 int m, int bb, long long groups) {
+    const long long total = groups * m * (long long)bb;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long g = i / ((long long)m * bb);
+        const long long b = i % bb;
+        parity[i] = data[g * bb + b];   // k = 1: the group holds one block
+    }
+}
+
+__global__ void rows_k1_kernel(const uint8_t* __restrict__ rows_in, uint8_t* rows_out,
+                               int32_t* __restrict__ status, long long groups) {
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= groups) return;
+    rows_out[g] = 0;
+    (void)rows_in;
+    if (status) status[g] = 0;
+}
+
+// ------------------------------------------------------------- bit-sliced GF apply
+// For one input block, the lane holds its column word of the 8 sub-rows, W[0..7].
+// Extend to W[n] = <alpha^n, in> for n = 0..14 (linear in the input):
+//   alpha^(n) = alpha^(n-1) + alpha^(n-6) + alpha^(n-7) + alpha^(n-8)   (from 0x187)
+// and keep the pair sums Z[n] = W[n] ^ W[n+1].  A coefficient a = sum_b a_b alpha^b then
+// contributes  out[r] ^= XOR_{b : a_b} W[b + r]   (r = 0..7), i.e. per nibble p of a at
+// bit offset B a fixed XOR of at most two W/Z terms per output sub-row.
+struct WZ {
+    uint32_t W[15];
+    uint32_t Z[14];
+};
+
+__device__ __forceinline__ void expand_wz(WZ& v) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) v.Z[i] = v.W[i] ^ v.W[i + 1];
+#pragma unroll
+    for (int n = 8; n < 15; ++n) v.W[n] = xor3(v.W[n - 1], v.W[n - 6], v.Z[n - 8]);
+#pragma unroll
+    for (int i = 7; i < 14; ++i) v.Z[i] = v.W[i] ^ v.W[i + 1];
+}
+
+template <int B>
+__device__ __forceinline__ void apply_nibble(uint32_t (&acc)[8], uint32_t p, const WZ& v) {
+#define QF_CASE(P, EXPR)                                   \
+    case P:                                                \
+        _Pragma("unroll") for (int r = 0; r < 8; ++r) { acc[r] = EXPR; } \
+        break;
+    switch (p) {
+        QF_CASE(1, acc[r] ^ v.W[B + r])
+        QF_CASE(2, acc[r] ^ v.W[B + 1 + r])
+        QF_CASE(3, acc[r] ^ v.Z[B + r])
+        QF_CASE(4, acc[r] ^ v.W[B + 2 + r])
+        QF_CASE(5, xor3(acc[r], v.W[B + r], v.W[B + 2 + r]))
+        QF_CASE(6, acc[r] ^ v.Z[B + 1 + r])
+        QF_CASE(7, xor3(acc[r], v.Z[B + r], v.W[B + 2 + r]))
+        QF_CASE(8, acc[r] ^ v.W[B + 3 + r])
+        QF_CASE(9, xor3(acc[r], v.W[B + r], v.W[B + 3 + r]))
+        QF_CASE(10, xor3(acc[r], v.W[B + 1 + r], v.W[B + 3 + r]))
+        QF_CASE(11, xor3(acc[r], v.Z[B + r], v.W[B + 3 + r]))
+        QF_CASE(12, acc[r] ^ v.Z[B + 2 + r])
+        QF_CASE(13, xor3(acc[r], v.W[B + r], v.Z[B + 2 + r]))
+        QF_CASE(14, xor3(acc[r], v.Z[B + 1 + r], v.W[B + 3 + r]))
+        QF_CASE(15, xor3(acc[r], v.Z[B + r], v.Z[B + 2 + r]))
+        default: break;
+    }
+#undef QF_CASE
+}
+
+// Column-word access.  Word c of sub-row t covers bytes [t*s + 4c, +4); the last word of a
+// sub-row may be partial (s % 4 != 0).  Loads of the last word are shifted back inside the
+// sub-row (never past the block) and realigned; stores write only the valid bytes.
+struct ColAccess {
+    int lo;        // byte offset of the dword actually loaded within the sub-row
+    int shift;     // right shift (bits) that realigns it
+    int nvalid;    // valid bytes of this lane's word (0 = lane idle)
+};
+
+template <bool TINY>
+__device__ __forceinline__ ColAccess col_access(int c, int nw, int s) {
+    ColAccess a;
+    const int cc = c < nw ? c : nw - 1;
+    const int off = 4 * cc;
+    a.nvalid = c < nw ? min(4, s - off) : 0;
+    if (!TINY) {
+        a.lo = min(off, s - 4);
+        a.shift = 8 * (off - a.lo);
+    } else {
+        a.lo = 0;
+        a.shift = 0;
+    }
+    return a;
+}
+
+// TINY = blocks under 32 bytes (s < 4): bytewise, never past the sub-row.  Otherwise the
+// raw (unshifted) dword; the caller applies `>> shift`.
+template <bool TINY>
+__device__ __forceinline__ uint32_t load_raw(const uint8_t* sub, const ColAccess& a, int s) {
+    if (!TINY) return *(const u32ua*)(sub + a.lo);
+    uint32_t v = 0;
+    for (int b = 0; b < 3; ++b)
+        if (b < s) v |= (uint32_t)sub[b] << (8 * b);
+    return v;
+}
+
+__device__ __forceinline__ void store_word(uint8_t* sub, int c, const ColAccess& a, uint32_t v) {
+    if (a.nvalid == 4) {
+        *(u32ua*)(sub + 4 * c) = v;
+    } else if (a.nvalid > 0) {
+        for (int b = 0; b < a.nvalid; ++b) sub[4 * c + b] = (uint8_t)(v >> (8 * b));
+    }
+}
+
+// One wave = one (group, output chunk, 64-word column tile).  RC outputs per wave.
+//   coef:  [(g) * coef_gstride + (chunk * k + pos) * RCP + j]  (RCP = max(4, RC))
+//   encode: outputs o = chunk*RC + j < m go to out + g*out_gstride + o*bb
+//   decode: outputs o < nout[g] go to out + g*out_gstride + slots[g*rmax + o]*bb
+template <int RC, bool DECODE, bool TINY>
+__global__ __launch_bounds__(256) void gf_apply_kernel(
+    const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ coef,
+    const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, int k, int m, int bb,
+    int nw, int ntiles, int nchunk, int rmax, long long coef_gstride, long long out_gstride,
+    int total_units) {
+    constexpr int RCP = RC < 4 ? 4 : RC;
+    constexpr int NCW = RCP / 4;
+    const int lane = threadIdx.x & 63;
+    const int unit = blockIdx.x * 4 + wave_id();
+    if (unit >= total_units) return;
+    const int tile = unit % ntiles;
+    const int gc = unit / ntiles;
+    const int chunk = gc % nchunk;
+    const int g = gc / nchunk;
+    int n = DECODE ? nout[g] : m;
+    n = min(n - chunk * RC, RC);
+    if (n <= 0) return;
+    const int s = bb >> 3;
+    const int c = tile * 64 + lane;
+    const ColAccess ca = col_access<TINY>(c, nw, s);
+
+    const uint8_t* gin = in + (long long)g * k * bb;
+    const uint32_t* cw = (const uint32_t*)(coef + (long long)g * coef_gstride +
+                                           (long long)chunk * k * RCP);
+
+    uint32_t acc[RC][8];
+#pragma unroll
+    for (int j = 0; j < RC; ++j)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc[j][r] = 0;
+
+    // Software pipeline: block pos+1's raw words and coefficients are in flight while
+    // block pos is combined (the realigning shift is applied at use, so the compiler's
+    // vmcnt wait lands in the next iteration).
+    uint32_t raw[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) raw[t] = load_raw<TINY>(gin + t * s, ca, s);
+    uint32_t cwn[NCW];
+#pragma unroll
+    for (int q = 0; q < NCW; ++q) cwn[q] = cw[q];
+
+#pragma unroll 1
+    for (int pos = 0; pos < k; ++pos) {
+        WZ v;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v.W[t] = TINY ? raw[t] : (raw[t] >> ca.shift);
+        uint32_t cwv[NCW];
+#pragma unroll
+        for (int q = 0; q < NCW; ++q) cwv[q] = cwn[q];
+        const int pn = pos + 1 < k ? pos + 1 : pos;   // clamped: no branch around the loads
+        const uint8_t* p = gin + (long long)pn * bb;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) raw[t] = load_raw<TINY>(p + t * s, ca, s);
+#pragma unroll
+        for (int q = 0; q < NCW; ++q) cwn[q] = cw[pn * NCW + q];
+        expand_wz(v);
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+            if (j < n) {
+                const uint32_t a = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                apply_nibble<0>(acc[j], a & 15u, v);
+                apply_nibble<4>(acc[j], a >> 4, v);
+            }
+        }
+    }
+
+#pragma unroll
+    for (int j = 0; j < RC; ++j) {
+        if (j < n) {
+            const int o = chunk * RC + j;
+            const int slot = (DECODE && slots) ? slots[(long long)g * rmax + o] : o;
+            uint8_t* dst = out + (long long)g * out_gstride + (long long)slot * bb;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) store_word(dst + r * s, c, ca, acc[j][r]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------- decode prep
+// One 64-lane workgroup per group.  Restates the reference's decode bookkeeping
+// (sort_blocks :543-575, erasure list, recovery row rewrite :791) and replaces its GF(2)
+// bitmatrix elimination by a GF(256) Gauss-Jordan inverse of the r x r erasure submatrix
+// S[i][j] = C[y_i][e_j]: since c -> (8x8 expansion) is a ring homomorphism, the inverse
+// bitmatrix is the expansion of S^-1, and the recovered data is unique.  Output rows:
+//   recovered e_j = sum_i Sinv[j][i] * R_i + sum_{x present} (sum_i Sinv[j][i] C[y_i][x]) * D_x
+// so one coefficient per (j, input slot) and a single pass over the received blocks.
+__global__ __launch_bounds__(64) void decode_prep_kernel(
+    const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
+    const uint8_t* __restrict__ cenc, uint8_t* __restrict__ coef, uint8_t* __restrict__ slots,
+    int32_t* __restrict__ nout, int k, int m, int bb, int rc, int rmax, int nchunk) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* gexp = smem;              // 512
+    uint8_t* glog = gexp + 512;        // 256
+    uint8_t* rowl = glog + 256;        // 256
+    uint8_t* present = rowl + 256;     // 256
+    uint8_t* recpos = present + 256;   // 256: slot of recovery i
+    uint8_t* era = recpos + 256;       // 256: erased row j
+    uint8_t* recidx = era + 256;       // 256: recovery index of slot (255 = original)
+    uint8_t* mat = recidx + 256;       // rmax x (2 rmax)
+    const int lane = threadIdx.x;
+    const long long g = blockIdx.x;
+    const int rcp = rc < 4 ? 4 : rc;
+
+    for (int i = lane; i < 512; i += 64) gexp[i] = c_gf.exp[i];
+    for (int i = lane; i < 256; i += 64) {
+        glog[i] = c_gf.log[i];
+        present[i] = 0;
+        recidx[i] = 255;
+    }
+    const uint8_t* rg = rows_in + g * k;
+    uint8_t* ro = rows_out + g * k;
+    for (int i = lane; i < k; i += 64) rowl[i] = rg[i];
+    __syncthreads();
+    for (int i = lane; i < k; i += 64)
+        if (rowl[i] < k) present[rowl[i]] = 1;
+    __syncthreads();
+
+    // recovery blocks in array order (sort_blocks)
+    int nrec = 0;
+    for (int base = 0; base < k; base += 64) {
+        const int i = base + lane;
+        const bool isrec = i < k && rowl[i] >= k;
+        const unsigned long long msk = __ballot(isrec);
+        const int pre = __popcll(msk & ((1ull << lane) - 1));
+        if (isrec) {
+            recpos[nrec + pre] = (uint8_t)i;
+            recidx[i] = (uint8_t)(nrec + pre);
+        }
+        nrec += __popcll(msk);
+    }
+    // erasures: the first nrec data rows not present, ascending
+    int nera = 0;
+    for (int base = 0; base < k && nera < nrec; base += 64) {
+        const int x = base + lane;
+        const bool miss = x < k && !present[x];
+        const unsigned long long msk = __ballot(miss);
+        const int pre = __popcll(msk & ((1ull << lane) - 1));
+        if (miss && nera + pre < nrec) era[nera + pre] = (uint8_t)x;
+        nera += __popcll(msk);
+    }
+    __syncthreads();
+
+    auto finish_unchanged = [&](int st) {
+        if (ro != rg)
+            for (int i = lane; i < k; i += 64) ro[i] = rowl[i];
+        if (lane == 0) {
+            nout[g] = 0;
+            if (status) status[g] = st;
+        }
+    };
+    if (nrec == 0) { finish_unchanged(0); return; }                       // :1287-1289
+    if (k + m > 256 || (bb & 7)) { finish_unchanged(-1); return; }        // :1292-1294
+    if (nrec > rmax || nera < nrec) { finish_unchanged(-3); return; }     // malformed rows
+    const int n = nrec;
+    const int n2 = 2 * n;
+    bool bad = false;
+    for (int i = 0; i < n; ++i)
+        if (rowl[recpos[i]] - k >= m) bad = true;                          // row >= k + m
+    if (bad) { finish_unchanged(-3); return; }
+
+    // [S | I]
+    for (int idx = lane; idx < n * n2; idx += 64) {
+        const int i = idx / n2, j = idx % n2;
+        uint8_t v;
+        if (j < n) v = cenc[(rowl[recpos[i]] - k) * k + era[j]];
+        else v = (j - n == i) ? 1 : 0;
+        mat[i * n2 + j] = v;
+    }
+    __syncthreads();
+    auto mul = [&](uint8_t a, uint8_t b) -> uint8_t {
+        return (a && b) ? gexp[glog[a] + glog[b]] : 0;
+    };
+    for (int p = 0; p < n; ++p) {
+        int piv = -1;
+        for (int base = p; base < n && piv < 0; base += 64) {
+            const int i = base + lane;
+            const unsigned long long msk = __ballot(i < n && mat[i * n2 + p] != 0);
+            if (msk) piv = base + __ffsll((long long)msk) - 1;
+        }
+        if (piv < 0) { finish_unchanged(-3); return; }                     // singular
+        if (piv != p) {
+            for (int j = lane; j < n2; j += 64) {
+                const uint8_t t = mat[p * n2 + j];
+                mat[p * n2 + j] = mat[piv * n2 + j];
+                mat[piv * n2 + j] = t;
+            }
+            __syncthreads();
+        }
+        const uint8_t inv = gexp[255 - glog[mat[p * n2 + p]]];
+        __syncthreads();
+        for (int j = lane; j < n2; j += 64) mat[p * n2 + j] = mul(mat[p * n2 + j], inv);
+        __syncthreads();
+        for (int i = 0; i < n; ++i) {
+            if (i == p) continue;
+            const uint8_t f = mat[i * n2 + p];
+            __syncthreads();
+            if (f)
+                for (int j = lane; j < n2; j += 64) mat[i * n2 + j] ^= mul(f, mat[p * n2 + j]);
+            __syncthreads();
+        }
+    }
+
+    // recovery coefficients per (output j, input slot pos)
+    for (int pos = lane; pos < k; pos += 64) {
+        const int ri = recidx[pos];
+        for (int j = 0; j < n; ++j) {
+            const uint8_t* inv_row = mat + j * n2 + n;   // Sinv[j][*]
+            uint8_t cval;
+            if (ri != 255) {
+                cval = inv_row[ri];
+            } else {
+                const int x = rowl[pos];
+                cval = 0;
+                for (int i = 0; i < n; ++i)
+                    cval ^= mul(inv_row[i], cenc[(rowl[recpos[i]] - k) * k + x]);
+            }
+            const int ch = j / rc, jj = j % rc;
+            coef[g * (long long)nchunk * k * rcp + ((long long)ch * k + pos) * rcp + jj] = cval;
+        }
+    }
+    if (ro != rg)
+        for (int i = lane; i < k; i += 64) ro[i] = rowl[i];
+    __syncthreads();
+    for (int j = lane; j < n; j += 64) {
+        slots[g * rmax + j] = recpos[j];
+        ro[recpos[j]] = era[j];                                            // :791
+    }
+    if (lane == 0) {
+        nout[g] = n;
+        if (status) status[g] = 0;
+    }
+}
+
+// In-place decode with more recovered blocks than one wave holds: the chunks write to a
+// [G][rmax][bb] scratch, then this copies each recovered block into its slot.
+__global__ __launch_bounds__(256) void scatter_recovered_kernel(
+    const uint8_t* __restrict__ scratch, uint8_t* __restrict__ out,
+    const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, int k, int bb,
+    int rmax, long long units) {
+    const long long u = (long long)blockIdx.x * 4 + wave_id();
+    if (u >= units) return;
+    const long long g = u / rmax;
+    const int o = (int)(u % rmax);
+    if (o >= nout[g]) return;
+    const int lane = threadIdx.x & 63;
+    const uint8_t* from = scratch + u * (long long)bb;
+    uint8_t* to = out + (g * k + slots[g * rmax + o]) * (long long)bb;
+    for (int q = lane; q < bb; q += 64) to[q] = from[q];
+}
+
+// ----------------------------------------------------------------------- synth
+__device__ __forceinline__ uint64_t splitmix64_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ void synth_fill_kernel(uint8_t* __restrict__ dst, unsigned long long bytes,
+                                  unsigned long long seed, unsigned long long off) {
+    // requires off % 8 == 0; word i of dst = stream word off/8 + i
+    const unsigned long long nwords = bytes / 8;
+    const unsigned long long w0 = off / 8;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+         i < nwords; i += (unsigned long long)gridDim.x * blockDim.x)
+        ((uint64_t*)dst)[i] = splitmix64_mix(seed + (w0 + i + 1) * 0x9E3779B97F4A7C15ULL);
+    const unsigned long long tail = bytes - nwords * 8;
+    if (blockIdx.x == 0 && threadIdx.x < tail) {
+        const uint64_t w = splitmix64_mix(seed + (w0 + nwords + 1) * 0x9E3779B97F4A7C15ULL);
+        dst[nwords * 8 + threadIdx.x] = (uint8_t)(w >> (8 * threadIdx.x));
+    }
+}
+
+__global__ __launch_bounds__(256) void synth_gather_kernel(
+    const uint8_t* __restrict__ data, const uint8_t* __restrict__ parity,
+    const int16_t* __restrict__ src, uint8_t* __restrict__ blocks, int k, int m, int bb,
+    long long units) {
+    const long long u = (long long)blockIdx.x * 4 + wave_id();
+    if (u >= units) return;
+    const int lane = threadIdx.x & 63;
+    const long long g = u / k;
+    const int sidx = src[u];
+    const uint8_t* from = sidx < k ? data + (g * k + sidx) * (long long)bb
+                                   : parity + (g * m + (sidx - k)) * (long long)bb;
+    uint8_t* to = blocks + u * (long long)bb;
+    if ((bb & 7) == 0) {
+        for (int q = lane; q < bb / 8; q += 64) ((u64a*)to)[q] = ((const u64a*)from)[q];
+    } else {
+        for (int q = lane; q < bb; q += 64) to[q] = from[q];
+    }
+}
+
+// ---------------------------------------------------------------------- launchers
+static inline unsigned blocks_for_waves(long long waves) { return (unsigned)((waves + 3) / 4); }
+
+static int xor_variant(const void* a, const void* b, int bb) {
+    // 0: 16B aligned-16, 1: 16B aligned-8, 2: 8B, 3: 4B, 4: 1B
+    const uintptr_t al = (uintptr_t)a | (uintptr_t)b | (uintptr_t)bb;
+    static int forced = -2;
+    if (forced == -2) {
+        const char* e = getenv("QFEC_XOR_VARIANT");
+        forced = e ? atoi(e) : -1;
+    }
+    int v;
+    if ((al & 15) == 0) v = 0;
+    else if ((al & 7) == 0) v = 1;
+    else if ((al & 3) == 0) v = 3;
+    else v = 4;
+    if (forced >= 0 && forced >= v) v = forced;   // may only relax alignment
+    return v;
+}
+
+template <int V>
+static void xor_encode_dispatch(const uint8_t* d, uint8_t* p, int k, int bb, long long G,
+                                long long os, hipStream_t st) {
+    const unsigned nb = blocks_for_waves(G);
+    switch (k) {
+        case 10: xor_encode_kernel<V, 10><<<nb, 256, 0, st>>>(d, p, k, bb, G, os); break;
+        case 5: xor_encode_kernel<V, 5><<<nb, 256, 0, st>>>(d, p, k, bb, G, os); break;
+        case 32: xor_encode_kernel<V, 32><<<nb, 256, 0, st>>>(d, p, k, bb, G, os); break;
+        default: xor_encode_kernel<V, 0><<<nb, 256, 0, st>>>(d, p, k, bb, G, os); break;
+    }
+}
+
+hipError_t launch_xor_encode(const uint8_t* data, uint8_t* parity, int k, int bb,
+                             long long groups, long long out_gstride, hipStream_t st) {
+    if (groups <= 0) return hipSuccess;
+    switch (xor_variant(data, parity, (int)(bb | out_gstride))) {
+        case 0: xor_encode_dispatch<0>(data, parity, k, bb, groups, out_gstride, st); break;
+        case 1: xor_encode_dispatch<1>(data, parity, k, bb, groups, out_gstride, st); break;
+        case 2: xor_encode_dispatch<2>(data, parity, k, bb, groups, out_gstride, st); break;
+        case 3: xor_encode_dispatch<3>(data, parity, k, bb, groups, out_gstride, st); break;
+        default: xor_encode_dispatch<4>(data, parity, k, bb, groups, out_gstride, st); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t* rows_in,
+                             uint8_t* rows_out, int32_t* status, int k, int bb,
+                             long long groups, hipStream_t st) {
+    if (groups <= 0) return hipSuccess;
+    const unsigned nb = blocks_for_waves(groups);
+    switch (xor_variant(blocks, out, bb)) {
+        case 0: xor_decode_kernel<0><<<nb, 256, 0, st>>>(blocks, out, rows_in, rows_out, status, k, bb, groups); break;
+        case 1: xor_decode_kernel<1><<<nb, 256, 0, st>>>(blocks, out, rows_in, rows_out, status, k, bb, groups); break;
+        case 2: xor_decode_kernel<2><<<nb, 256, 0, st>>>(blocks, out, rows_in, rows_out, status, k, bb, groups); break;
+        case 3: xor_decode_kernel<3><<<nb, 256, 0, st>>>(blocks, out, rows_in, rows_out, status, k, bb, groups); break;
+        default: xor_decode_kernel<4><<<nb, 256, 0, st>>>(blocks, out, rows_in, rows_out, status, k, bb, groups); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_replicate(const uint8_t* data, uint8_t* parity, int m, int bb,
+                            long long groups, hipStream_t st) {
+    if (groups <= 0 || m <= 0) return hipSuccess;
+    const long long total = groups * m * (long long)bb;
+    const unsigned nb = (unsigned)std::min<long long>((total + 255) / 256, 65536);
+    replicate_kernel<<<nb, 256, 0, st>>>(data, parity, m, bb, groups);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_k1(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
+                          long long groups, hipStream_t st) {
+    if (groups <= 0) return hipSuccess;
+    rows_k1_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(rows_in, rows_out, status,
+                                                                     groups);
+    return hipGetLastError();
+}
+
+template <bool DECODE>
+static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8_t* coef,
+                                    const uint8_t* slots, const int32_t* nout, int k, int m,
+                                    int bb, long long groups, int rc, int nchunk, int rmax,
+                                    long long coef_gstride, long long out_gstride,
+                                    hipStream_t st) {
+    const int s = bb / 8;
+    const int nw = (s + 3) / 4;
+    const int ntiles = (nw + 63) / 64;
+    const long long units = groups * nchunk * ntiles;
+    if (units <= 0) return hipSuccess;
+    if (units > 0x7fffffffLL) return hipErrorInvalidValue;
+    const unsigned nb = blocks_for_waves(units);
+    const int tu = (int)units;
+#define QF_LAUNCH(RCV)                                                                        \
+    do {                                                                                      \
+        if (s >= 4)                                                                           \
+            gf_apply_kernel<RCV, DECODE, false><<<nb, 256, 0, st>>>(                          \
+                in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
+                out_gstride, tu);                                                             \
+        else                                                                                  \
+            gf_apply_kernel<RCV, DECODE, true><<<nb, 256, 0, st>>>(                           \
+                in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
+                out_gstride, tu);                                                             \
+    } while (0)
+    switch (rc) {
+        case 1: QF_LAUNCH(1); break;
+        case 2: QF_LAUNCH(2); break;
+        case 4: QF_LAUNCH(4); break;
+        case 8: QF_LAUNCH(8); break;
+        case 16: QF_LAUNCH(16); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef QF_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t* coef, int k,
+                            int m, int bb, long long groups, int rc, hipStream_t st) {
+    const int nchunk = (m + rc - 1) / rc;
+    return gf_apply_dispatch<false>(data, parity, coef, nullptr, nullptr, k, m, bb, groups, rc,
+                                    nchunk, 0, 0, (long long)m * bb, st);
+}
+
+hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
+                              const uint8_t* cenc, DecodeWork w, int k, int m, int bb, int rc,
+                              int rmax, long long groups, hipStream_t st) {
+    if (groups <= 0) return hipSuccess;
+    if (groups > 0x7fffffffLL) return hipErrorInvalidValue;
+    const int nchunk = (rmax + rc - 1) / rc;
+    const size_t lds = 512 + 256 * 6 + (size_t)rmax * 2 * rmax;
+    decode_prep_kernel<<<(unsigned)groups, 64, lds, st>>>(rows_in, rows_out, status, cenc,
+                                                          w.coef, w.slots, w.nout, k, m, bb,
+                                                          rc, rmax, nchunk);
+    return hipGetLastError();
+}
+
+hipError_t launch_gf_decode(const uint8_t* blocks, uint8_t* out, DecodeWork w, int k, int m,
+                            int bb, long long groups, int rc, int rmax, hipStream_t st) {
+    const int nchunk = (rmax + rc - 1) / rc;
+    const int rcp = rc < 4 ? 4 : rc;
+    return gf_apply_dispatch<true>(blocks, out, w.coef, w.slots, w.nout, k, m, bb, groups, rc,
+                                   nchunk, rmax, (long long)nchunk * k * rcp,
+                                   (long long)k * bb, st);
+}
+
+hipError_t launch_scatter_recovered(const uint8_t* scratch, uint8_t* out, DecodeWork w, int k,
+                                   int bb, int rmax, long long groups, hipStream_t st) {
+    const long long units = groups * rmax;
+    if (units <= 0) return hipSuccess;
+    scatter_recovered_kernel<<<blocks_for_waves(units), 256, 0, st>>>(scratch, out, w.slots,
+                                                                      w.nout, k, bb, rmax,
+                                                                      units);
+    return hipGetLastError();
+}
+
+hipError_t launch_gf_decode_scratch(const uint8_t* blocks, uint8_t* scratch, DecodeWork w,
+                                   int k, int m, int bb, long long groups, int rc, int rmax,
+                                   hipStream_t st) {
+    const int nchunk = (rmax + rc - 1) / rc;
+    const int rcp = rc < 4 ? 4 : rc;
+    return gf_apply_dispatch<true>(blocks, scratch, w.coef, nullptr, w.nout, k, m, bb, groups,
+                                   rc, nchunk, rmax, (long long)nchunk * k * rcp,
+                                   (long long)rmax * bb, st);
+}
+
+hipError_t launch_synth_fill(uint8_t* dst, unsigned long long bytes, unsigned long long seed,
+                             unsigned long long byte_offset, hipStream_t st) {
+    if (bytes == 0) return hipSuccess;
+    if (byte_offset % 8) return hipErrorInvalidValue;
+    const unsigned long long words = bytes / 8 + 1;
+    const unsigned nb = (unsigned)std::min<unsigned long long>((words + 255) / 256, 1u << 16);
+    synth_fill_kernel<<<nb, 256, 0, st>>>(dst, bytes, seed, byte_offset);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_gather(const uint8_t* data, const uint8_t* parity, const int16_t* src,
+                               uint8_t* blocks, int k, int m, int bb, long long groups,
+                               hipStream_t st) {
+    const long long units = groups * k;
+    if (units <= 0) return hipSuccess;
+    synth_gather_kernel<<<blocks_for_waves(units), 256, 0, st>>>(data, parity, src, blocks, k,
+                                                                 m, bb, units);
+    return hipGetLastError();
+}
+
+}  // namespace qfec

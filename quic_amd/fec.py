@@ -1,0 +1,190 @@
+"""Python front-end of the MI355X FEC engine (ctypes over libquic_fec.so).
+
+Mirrors the reference codec interface (net/quic/core/libcat/cauchy_256.h):
+`cauchy_256_init`, `cauchy_256_encode`, `cauchy_256_decode`, `Block`, with the same
+argument meaning, return codes and in-place decode semantics, plus the batched
+engine (`FecEngine`) that the GPU path is built for.  Every byte of parity or
+recovered data is computed by the gfx950 kernels; nothing here computes on the CPU.
+
+Device buffers are torch tensors (uint8, contiguous, on a ROCm device): torch is
+used only for memory and streams.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import Block, FecError, load
+
+CAUCHY_256_VERSION = 2
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+# ----------------------------------------------------------------- reference ABI
+def _cauchy_256_init(expected_version):
+    """cauchy_256.h:47.  0 on success, -1 on a version mismatch (what the reference
+    code returns), negative on GPU bring-up failure."""
+    return load()._cauchy_256_init(expected_version)
+
+
+def cauchy_256_init():
+    return _cauchy_256_init(CAUCHY_256_VERSION)
+
+
+def _as_u8(a):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    return a, a.ctypes.data_as(_u8p)
+
+
+def cauchy_256_encode(k, m, data_ptrs, recovery_blocks, block_bytes):
+    """cauchy_256.h:78.  data_ptrs: sequence of k uint8 arrays (block_bytes each);
+    recovery_blocks: writable uint8 array of m*block_bytes bytes (filled in place).
+    Returns the reference's return code."""
+    keep = [_as_u8(d) for d in data_ptrs]
+    arr = (_u8p * max(len(keep), 1))(*[p for _, p in keep])
+    if not (isinstance(recovery_blocks, np.ndarray) and recovery_blocks.dtype == np.uint8
+            and recovery_blocks.flags.c_contiguous):
+        raise TypeError("recovery_blocks must be a C-contiguous uint8 numpy array")
+    return load().cauchy_256_encode(k, m, arr, recovery_blocks.ctypes.data_as(ctypes.c_void_p),
+                                    block_bytes)
+
+
+def make_blocks(arrays, rows):
+    """Build a `Block[]` over caller-owned uint8 arrays (decoded in place)."""
+    blocks = (Block * max(len(arrays), 1))()
+    for i, (a, r) in enumerate(zip(arrays, rows)):
+        if not (isinstance(a, np.ndarray) and a.dtype == np.uint8 and a.flags.c_contiguous):
+            raise TypeError("blocks must be C-contiguous uint8 numpy arrays")
+        blocks[i].data = a.ctypes.data_as(_u8p)
+        blocks[i].row = int(r)
+    return blocks
+
+
+def cauchy_256_decode(k, m, blocks, block_bytes):
+    """cauchy_256.h:103.  `blocks` is a Block array from make_blocks(); data and row
+    fields are updated in place.  Returns the reference's return code."""
+    return load().cauchy_256_decode(k, m, blocks, block_bytes)
+
+
+def cauchy_matrix(k, m):
+    """Rows 1..m-1 of the Cauchy matrix the reference uses, (m-1) x k."""
+    out = np.zeros((m - 1, k), np.uint8)
+    rc = load().qfec_cauchy_matrix(k, m, out.ctypes.data_as(ctypes.c_void_p))
+    if rc:
+        raise ValueError(f"no Cauchy matrix for k={k} m={m}")
+    return out
+
+
+# ------------------------------------------------------------------ batch engine
+def _dptr(t):
+    if t is None:
+        return None
+    import torch
+    if not isinstance(t, torch.Tensor):
+        raise TypeError("device buffers must be torch tensors")
+    if not t.is_cuda or t.dtype not in (torch.uint8, torch.int8, torch.int16, torch.int32):
+        raise TypeError("device buffers must be integer tensors on a ROCm device")
+    if not t.is_contiguous():
+        raise ValueError("device buffers must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream, like):
+    if stream is not None:
+        return ctypes.c_void_p(int(stream))
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(like.device).cuda_stream)
+
+
+class FecEngine:
+    """One per GPU: owns a qfec_ctx (coefficient tables, decode workspace, staging)."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        self.device = device
+        h = ctypes.c_void_p()
+        rc = self.lib.qfec_ctx_create(device, ctypes.byref(h))
+        if rc:
+            raise FecError(rc, "qfec_ctx_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.qfec_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, k, m, block_bytes, groups):
+        rc = self.lib.qfec_reserve(self._h, k, m, block_bytes, groups)
+        if rc:
+            raise FecError(rc, "qfec_reserve")
+
+    # device-resident batch calls (enqueue only)
+    def encode(self, k, m, block_bytes, data, parity, stream=None):
+        """data [G][k][bb] -> parity [G][m][bb] (torch uint8 on the device).  Returns
+        0 or -1 (the reference's unsupported-parameter code)."""
+        G = data.shape[0]
+        rc = self.lib.qfec_encode_batch(self._h, k, m, block_bytes, G, _dptr(data),
+                                        _dptr(parity), _stream(stream, data))
+        if rc < -1:
+            raise FecError(rc, "qfec_encode_batch")
+        return rc
+
+    def decode(self, k, m, block_bytes, blocks, rows_in, out=None, rows_out=None, status=None,
+               stream=None):
+        """blocks [G][k][bb], rows_in [G][k] uint8.  out defaults to blocks (in place),
+        rows_out to rows_in.  status: optional int32 [G]."""
+        G = blocks.shape[0]
+        out = blocks if out is None else out
+        rows_out = rows_in if rows_out is None else rows_out
+        rc = self.lib.qfec_decode_batch(self._h, k, m, block_bytes, G, _dptr(blocks),
+                                        _dptr(rows_in), _dptr(out), _dptr(rows_out),
+                                        _dptr(status), _stream(stream, blocks))
+        if rc:
+            raise FecError(rc, "qfec_decode_batch")
+        return rc
+
+    # host-pointer batch calls (synchronous; include H2D/D2H)
+    def encode_host(self, k, m, block_bytes, data):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        G = data.shape[0]
+        parity = np.zeros((G, m, block_bytes), np.uint8)
+        rc = self.lib.qfec_encode_batch_host(self._h, k, m, block_bytes, G,
+                                             data.ctypes.data_as(ctypes.c_void_p),
+                                             parity.ctypes.data_as(ctypes.c_void_p))
+        if rc < -1:
+            raise FecError(rc, "qfec_encode_batch_host")
+        return parity, rc
+
+    def decode_host(self, k, m, block_bytes, blocks, rows):
+        blocks = np.array(blocks, dtype=np.uint8, order="C", copy=True)
+        rows = np.array(rows, dtype=np.uint8, order="C", copy=True)
+        G = blocks.shape[0]
+        status = np.zeros(G, np.int32)
+        rc = self.lib.qfec_decode_batch_host(self._h, k, m, block_bytes, G,
+                                             blocks.ctypes.data_as(ctypes.c_void_p),
+                                             rows.ctypes.data_as(ctypes.c_void_p),
+                                             status.ctypes.data_as(ctypes.c_void_p))
+        if rc:
+            raise FecError(rc, "qfec_decode_batch_host")
+        return blocks, rows, status
+
+
+def synth_fill(t, seed, byte_offset=0, stream=None):
+    """Fill a device tensor with the seeded splitmix64 stream (quic_amd.synth)."""
+    rc = load().qfec_synth_fill(_dptr(t), t.numel() * t.element_size(), seed, byte_offset,
+                                _stream(stream, t))
+    if rc:
+        raise FecError(rc, "qfec_synth_fill")
+
+
+def synth_gather(data, parity, src, blocks, k, m, block_bytes, stream=None):
+    """blocks[g][i] = sent block src[g][i] of group g (device-side receive-set build)."""
+    rc = load().qfec_synth_gather(_dptr(data), _dptr(parity), _dptr(src), _dptr(blocks), k, m,
+                                  block_bytes, data.shape[0], _stream(stream, data))
+    if rc:
+        raise FecError(rc, "qfec_synth_gather")

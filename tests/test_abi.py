@@ -1,0 +1,73 @@
+"""CPU: the C-ABI library loads and exports every symbol include/quic_fec.h declares;
+host-side tables match the oracle.  No compute calls (no GPU here)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from quic_amd import _lib, fec
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "quic_fec.h")) as f:
+        text = f.read()
+    return set(re.findall(r"^QFEC_API\s+[\w\s\*]*?\b(\w+)\s*\(", text, re.M))
+
+
+def test_library_exports_every_header_symbol():
+    syms = header_symbols()
+    assert {"_cauchy_256_init", "cauchy_256_encode", "cauchy_256_decode",
+            "qfec_encode_batch", "qfec_decode_batch"} <= syms
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert syms <= exported, syms - exported
+    # nothing else leaks out of the C ABI (internal kernels/launchers are hidden)
+    extra = {s for s in exported if not s.startswith(("_Z", "__")) and s not in syms}
+    assert not extra, extra
+
+
+def test_ctypes_signatures_cover_header():
+    assert header_symbols() <= set(_lib.SIGNATURES)
+    L = _lib.load()
+    for name in header_symbols():
+        assert getattr(L, name) is not None
+
+
+def test_block_struct_layout():
+    import ctypes
+    # cauchy_256.h:52-55: { unsigned char *data; unsigned char row; }
+    assert ctypes.sizeof(_lib.Block) == 16
+    assert _lib.Block.row.offset == 8
+
+
+def test_no_cpu_fallback_in_product():
+    # the product library must not link or embed the oracle
+    out = subprocess.run(["nm", "-D", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle_" not in out
+    ldd = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in ldd and "ref_cauchy" not in ldd
+    src = open(os.path.join(ROOT, "quic_amd", "fec.py")).read()
+    assert "oracle" not in src.replace("oracle/_ref", "")
+
+
+@pytest.mark.parametrize("k,m", [(32, 4), (10, 2), (10, 6), (128, 16), (10, 20), (250, 5),
+                                 (200, 56), (1, 255), (249, 7)])
+def test_cauchy_matrix_matches_oracle(oracle, k, m):
+    np.testing.assert_array_equal(fec.cauchy_matrix(k, m), oracle.cauchy_matrix(k, m))
+
+
+def test_cauchy_matrix_rejects_bad_params():
+    with pytest.raises(ValueError):
+        fec.cauchy_matrix(250, 7)
+    with pytest.raises(ValueError):
+        fec.cauchy_matrix(10, 1)
+
+
+def test_init_version_mismatch_is_minus_one():
+    # version check happens before any device access (cauchy_256.cpp:389-398)
+    assert fec._cauchy_256_init(1) == -1

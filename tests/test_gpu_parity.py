@@ -1,0 +1,227 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the golden vectors from
+the reference codec and against the CPU oracle, bit-exact.  Run with -m gpu."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from quic_amd import fec, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def gpu_encode(engine, k, m, bb, data):
+    import torch
+    d = dev(data)
+    p = torch.zeros((data.shape[0], m, bb), dtype=torch.uint8, device="cuda")
+    rc = engine.encode(k, m, bb, d, p)
+    return host(p), rc
+
+
+def gpu_decode(engine, k, m, bb, blocks, rows, inplace=True):
+    import torch
+    b = dev(blocks)
+    r = dev(rows)
+    st = torch.full((blocks.shape[0],), 7, dtype=torch.int32, device="cuda")
+    if inplace:
+        engine.decode(k, m, bb, b, r, status=st)
+        return host(b), host(r), host(st)
+    out = torch.zeros_like(b)
+    ro = torch.zeros_like(r)
+    engine.decode(k, m, bb, b, r, out=out, rows_out=ro, status=st)
+    # out-of-place: only recovered slots are written; merge for comparison
+    o = host(out)
+    rin = rows.astype(np.int64)
+    merged = blocks.copy()
+    mask = rin >= k
+    merged[mask] = o[mask]
+    return merged, host(ro), host(st)
+
+
+# ---------------------------------------------------------------- golden vectors
+def batch_case_ids(golden_cases):
+    return [c["name"] for c in golden_cases if c["kind"] == "batch"]
+
+
+@pytest.mark.parametrize("inplace", [True, False])
+def test_golden_batch_cases(engine, golden, inplace):
+    cases, full = golden
+    for c in cases:
+        if c["kind"] != "batch":
+            continue
+        k, m, bb, G = c["k"], c["m"], c["bb"], c["groups"]
+        data = synth.group_data(c["seed"], k, bb, G)
+        par, rc = gpu_encode(engine, k, m, bb, data)
+        assert rc == c["encode_rc"], c["name"]
+        assert sha(par) == c["parity_sha256"], c["name"]
+        rows = np.array(c["rows_in"], np.uint8)
+        recv = synth.assemble_received(data, par, rows.astype(np.int16))
+        out, rows_out, status = gpu_decode(engine, k, m, bb, recv, rows, inplace=inplace)
+        assert rows_out.tolist() == c["rows_out"], c["name"]
+        assert status.tolist() == c["status"], c["name"]
+        assert sha(out) == c["decoded_sha256"], c["name"]
+
+
+def test_golden_single_group_dropins(golden):
+    """cauchy_256_encode / cauchy_256_decode (the drop-in ABI) on the GPU."""
+    cases, full = golden
+    assert fec.cauchy_256_init() == 0
+    for c in cases:
+        k, m, bb = c.get("k"), c.get("m"), c.get("bb")
+        if c["kind"] == "encode":
+            blocks = [synth.stream_bytes(c["seed"], i * bb, bb) for i in range(k)]
+            out = np.zeros(m * bb, np.uint8)
+            rc = fec.cauchy_256_encode(k, m, blocks, out, bb)
+            assert rc == c["rc"], c["name"]
+            assert sha(out.reshape(m, bb)) == c["recovery_sha256"], c["name"]
+        elif c["kind"] == "decode":
+            blocks = [synth.stream_bytes(c["seed"], i * bb, bb) for i in range(k)]
+            blk = fec.make_blocks(blocks, c["rows_in"])
+            rc = fec.cauchy_256_decode(k, m, blk, bb)
+            assert rc == c["rc"], c["name"]
+            assert [blk[i].row for i in range(k)] == c["rows_out"], c["name"]
+            assert sha(np.stack(blocks)) == c["blocks_sha256"], c["name"]
+        elif c["kind"] == "batch" and c["groups"] * c["k"] * c["bb"] < 2_000_000:
+            # the batch cases through the per-group drop-in, group 0
+            k, m, bb = c["k"], c["m"], c["bb"]
+            data = synth.group_data(c["seed"], k, bb, 1)[0]
+            rec = np.zeros(m * bb, np.uint8)
+            rc = fec.cauchy_256_encode(k, m, list(data), rec, bb)
+            assert rc == c["encode_rc"]
+            full_par = full.get(c["name"] + "__parity")
+            if full_par is not None:
+                np.testing.assert_array_equal(rec.reshape(m, bb), full_par[0])
+            rows = c["rows_in"][0]
+            sent = np.concatenate([data, rec.reshape(m, bb)])
+            blocks = [sent[r].copy() for r in rows]
+            blk = fec.make_blocks(blocks, rows)
+            assert fec.cauchy_256_decode(k, m, blk, bb) == c["status"][0]
+            assert [blk[i].row for i in range(k)] == c["rows_out"][0]
+            for i in range(k):
+                np.testing.assert_array_equal(blocks[i], data[blk[i].row])
+
+
+# ----------------------------------------------------------- randomized vs oracle
+CONFIGS = [
+    # (k, m, bb, r, shuffle)
+    (10, 1, 1352, 1, False), (10, 1, 1350, 1, True), (10, 1, 1351, 1, False), (3, 1, 7, 1, True),
+    (10, 1, 1352, 0, False), (255, 1, 64, 1, False), (64, 1, 9008, 1, True),
+    (32, 4, 1352, 2, False), (32, 4, 1352, 4, True), (32, 4, 1352, 1, True), (32, 4, 1352, 0, False),
+    (2, 2, 8, 2, False), (5, 3, 16, 3, True), (7, 2, 24, 1, False), (9, 4, 40, 4, True),
+    (17, 5, 1352, 5, True), (16, 8, 9008, 8, False), (20, 10, 64, 10, True),
+    (128, 16, 1352, 8, False), (100, 20, 136, 17, True), (40, 40, 32, 33, True),
+    (200, 56, 16, 40, False), (250, 5, 1352, 5, False), (10, 15, 1352, 10, True),
+]
+
+
+@pytest.mark.parametrize("k,m,bb,r,shuffle", CONFIGS)
+def test_random_vs_oracle(engine, oracle, k, m, bb, r, shuffle):
+    G = 5
+    data = synth.group_data(1234 + k * 7 + m, k, bb, G)
+    p_or, rc_or = oracle.encode_batch(k, m, bb, data)
+    p_gpu, rc = gpu_encode(engine, k, m, bb, data)
+    assert rc == rc_or
+    np.testing.assert_array_equal(p_gpu, p_or)
+    rows, src = synth.loss_patterns(k, m, r, G, 77 + bb, shuffle=shuffle)
+    recv = synth.assemble_received(data, p_or, src)
+    b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+    for inplace in (True, False):
+        b, rr, s = gpu_decode(engine, k, m, bb, recv, rows, inplace=inplace)
+        np.testing.assert_array_equal(rr, r_or)
+        np.testing.assert_array_equal(s, s_or)
+        np.testing.assert_array_equal(b, b_or)
+
+
+def test_unsupported_params_status(engine, oracle):
+    # k + m > 256: encode writes P0 then returns -1; decode with erasures -> status -1
+    k, m, bb = 250, 7, 16
+    data = synth.group_data(5, k, bb, 3)
+    p_gpu, rc = gpu_encode(engine, k, m, bb, data)
+    p_or, rc_or = oracle.encode_batch(k, m, bb, data)
+    assert rc == rc_or == -1
+    np.testing.assert_array_equal(p_gpu, p_or)
+    rows = np.tile(np.array(list(range(1, 250)) + [250], np.uint8), (3, 1))
+    b, rr, s = gpu_decode(engine, k, m, bb, data, rows)
+    b2, rr2, s2 = oracle.decode_batch(k, m, bb, data, rows)
+    assert s.tolist() == s2.tolist() == [-1, -1, -1]
+    np.testing.assert_array_equal(rr, rr2)
+    np.testing.assert_array_equal(b, b2)
+    # block_bytes % 8 != 0 with m > 1
+    k, m, bb = 10, 3, 1350
+    data = synth.group_data(6, k, bb, 2)
+    p_gpu, rc = gpu_encode(engine, k, m, bb, data)
+    p_or, rc_or = oracle.encode_batch(k, m, bb, data)
+    assert rc == rc_or == -1
+    np.testing.assert_array_equal(p_gpu, p_or)
+
+
+def test_host_pointer_batch(engine, oracle):
+    k, m, bb, G, r = 32, 4, 1352, 64, 3
+    data = synth.group_data(42, k, bb, G)
+    par, rc = engine.encode_host(k, m, bb, data)
+    p_or, _ = oracle.encode_batch(k, m, bb, data)
+    assert rc == 0
+    np.testing.assert_array_equal(par, p_or)
+    rows, src = synth.loss_patterns(k, m, r, G, 3, shuffle=True)
+    recv = synth.assemble_received(data, par, src)
+    b, rr, s = engine.decode_host(k, m, bb, recv, rows)
+    b2, rr2, s2 = oracle.decode_batch(k, m, bb, recv, rows)
+    np.testing.assert_array_equal(b, b2)
+    np.testing.assert_array_equal(rr, rr2)
+    np.testing.assert_array_equal(s, s2)
+
+
+# ------------------------------------------------------ BASELINE-size properties
+@pytest.mark.parametrize("k,m,bb,r", [(10, 1, 1352, 1), (32, 4, 1352, 2)])
+def test_full_size_round_trip(engine, oracle, k, m, bb, r):
+    """65,536 groups (BASELINE.json configs[1], [2]): device-side synthetic data,
+    encode -> lose r data blocks per group -> decode; every recovered block must equal
+    the original, and sampled groups must match the oracle byte for byte."""
+    import torch
+    G = 65536
+    data = torch.empty((G, k, bb), dtype=torch.uint8, device="cuda")
+    fec.synth_fill(data, seed=2024)
+    parity = torch.zeros((G, m, bb), dtype=torch.uint8, device="cuda")
+    assert engine.encode(k, m, bb, data, parity) == 0
+    rows, src = synth.loss_patterns(k, m, r, G, 11, shuffle=False)
+    rows_d, src_d = dev(rows), dev(src)
+    blocks = torch.empty((G, k, bb), dtype=torch.uint8, device="cuda")
+    fec.synth_gather(data, parity, src_d, blocks, k, m, bb)
+    out = torch.zeros_like(blocks)
+    rows_out = torch.zeros_like(rows_d)
+    status = torch.full((G,), 9, dtype=torch.int32, device="cuda")
+    engine.decode(k, m, bb, blocks, rows_d, out=out, rows_out=rows_out, status=status)
+    torch.cuda.synchronize()
+    assert int(status.abs().max()) == 0
+    # recovered slots: rows_in >= k; their data must be data[g][rows_out]
+    rin = rows_d.long()
+    slot_mask = rin >= k
+    ro = rows_out.long()
+    assert bool((ro[slot_mask] < k).all())
+    g_idx = torch.arange(G, device="cuda")[:, None].expand(G, k)[slot_mask]
+    recovered = out[slot_mask]
+    original = data[g_idx, ro[slot_mask]]
+    assert torch.equal(recovered, original)
+    # the synthetic stream is the documented splitmix64 stream
+    np.testing.assert_array_equal(host(data[5]).ravel(),
+                                  synth.stream_bytes(2024, 5 * k * bb, k * bb))
+    # sampled groups vs the oracle
+    sample = [0, 1, 777, G - 1]
+    d_np = host(data[sample])
+    p_or, _ = oracle.encode_batch(k, m, bb, d_np)
+    np.testing.assert_array_equal(host(parity[sample]), p_or)
