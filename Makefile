@@ -11,10 +11,11 @@ TABLES  := $(ROOT)quic_amd/data/cauchy_256_tables.bin
 HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
+            -mllvm -structurizecfg-skip-uniform-regions=true \
             -DQFEC_BUILD -DQFEC_TABLES_PATH='"$(TABLES)"' -Wall -Wno-unused-function
 
 SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/fec_api.cpp
-HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(ROOT)include/quic_fec.h
+HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(ROOT)include/quic_fec.h $(ROOT)Makefile
 OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/fec_api.o
 
 .PHONY: all lib oracle clean

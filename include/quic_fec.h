@@ -63,8 +63,8 @@ QFEC_API int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes);
  *   data   [G][k][bb]   parity [G][m][bb]
  *   blocks [G][k][bb]   rows   [G][k]  (u8 row tags, data 0..k-1, parity k..k+m-1)
  *   status [G]          per-group return code of the equivalent cauchy_256_decode call
- * `stream` is a hipStream_t (NULL = the context's stream).  Device entry points only
- * enqueue work; they do not synchronise.
+ * `stream` is a hipStream_t (NULL = HIP's null stream, as everywhere in HIP).  Device
+ * entry points only enqueue work on that stream; they do not synchronise.
  * ------------------------------------------------------------------------------- */
 typedef struct qfec_ctx qfec_ctx;
 

@@ -97,7 +97,7 @@ int pow2_at_least(int v) {
     while (p < v) p <<= 1;
     return p;
 }
-int encode_rc(int m) { return std::min(pow2_at_least(m), 16); }
+int encode_rc(int m) { return std::min(pow2_at_least(m), 8); }
 int decode_rc(int rmax) { return std::min(pow2_at_least(rmax), 8); }
 
 struct DevBuf {
@@ -147,7 +147,9 @@ int set_device(qfec_ctx* c) {
     return 0;
 }
 
-hipStream_t pick(qfec_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+// A stream argument is a plain hipStream_t: NULL is HIP's null (default) stream, as
+// everywhere in HIP, so calls order with the caller's other work on that stream.
+hipStream_t pick(qfec_ctx*, void* s) { return (hipStream_t)s; }
 
 // Encode coefficient table: output o = chunk*rc + j; o == 0 is the all-ones row.
 int get_enc_table(qfec_ctx* c, int k, int m, int rc, const uint8_t** out) {
@@ -236,8 +238,9 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
         return 0;
     }
     if (m == 1) {   // :1264-1267
-        QF_HIP(qfec::launch_xor_decode(d_blocks, d_out, d_rows_in, d_rows_out, d_status, k, bb, G,
-                                       st));
+        QF_HIP(c->dslots.ensure((size_t)G));
+        QF_HIP(qfec::launch_xor_decode(d_blocks, d_out, d_rows_in, d_rows_out, d_status,
+                                       (uint8_t*)c->dslots.p, k, bb, G, st));
         return 0;
     }
     const int rmax = std::min(k, m);
@@ -251,7 +254,7 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc, rmax,
                                     G, st));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
-    if (nchunk > 1 && d_out == d_blocks) {
+    if (nchunk > 1 && d_out == d_blocks && !qfec::gf_staged(d_blocks, k, bb, nchunk, rc)) {
         // in place with several output chunks: a later chunk would read slots an earlier
         // chunk already overwrote, so stage the recovered blocks first
         QF_HIP(c->dscratch.ensure((size_t)G * rmax * bb));
@@ -504,6 +507,7 @@ int qfec_reserve(qfec_ctx* c, int k, int m, int bb, long long groups) {
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(c->mu);
     if ((rc = set_device(c))) return rc;
+    QF_HIP(c->dslots.ensure((size_t)groups));   // m == 1 decode: erased slot per group
     if (m > 1 && k > 1 && k + m <= 256) {
         const uint8_t* t;
         if ((rc = get_enc_table(c, k, m, encode_rc(m), &t))) return rc;

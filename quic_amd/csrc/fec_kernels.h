@@ -24,9 +24,10 @@ struct DecodeWork {
 hipError_t launch_xor_encode(const uint8_t* data, uint8_t* parity, int k, int bb,
                              long long groups, long long out_gstride, hipStream_t st);
 
-// m == 1 decode: XOR the k-1 other blocks into the block tagged row >= k.
+// m == 1 decode: XOR the k-1 other blocks into the block tagged row >= k.  eidx is a
+// [G] byte workspace (erased slot per group).
 hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t* rows_in,
-                             uint8_t* rows_out, int32_t* status, int k, int bb,
+                             uint8_t* rows_out, int32_t* status, uint8_t* eidx, int k, int bb,
                              long long groups, hipStream_t st);
 
 // k <= 1 encode: copy data[0] into each of the m outputs (cauchy_256.cpp:1508-1516).
@@ -59,6 +60,9 @@ hipError_t launch_gf_decode_scratch(const uint8_t* blocks, uint8_t* scratch, Dec
                                    hipStream_t st);
 hipError_t launch_scatter_recovered(const uint8_t* scratch, uint8_t* out, DecodeWork w, int k,
                                    int bb, int rmax, long long groups, hipStream_t st);
+
+// Whether a decode of this shape runs the LDS-staged kernel (no in-place hazard).
+bool gf_staged(const void* in, int k, int bb, int nchunk, int rc);
 
 // Synthetic workload helpers (bench / tests): splitmix64 stream and receive-set gather.
 hipError_t launch_synth_fill(uint8_t* dst, unsigned long long bytes, unsigned long long seed,

@@ -29,8 +29,6 @@ namespace qfec {
 
 typedef uint32_t u32ua __attribute__((aligned(1)));   // unaligned dword (gfx950 unaligned mode)
 typedef uint64_t u64a __attribute__((aligned(8)));
-typedef uint32_t u32x4a16 __attribute__((ext_vector_type(4), aligned(16)));
-typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
 
 __constant__ GfTables c_gf = make_gf_tables();
 
@@ -43,107 +41,213 @@ __device__ __forceinline__ int wave_id() {
 }
 
 // ------------------------------------------------------------------ m = 1 XOR paths
-// Vector access policy: V is the per-lane access type.  Tail bytes (bb % sizeof(V)) are
-// handled bytewise by the first lanes.
-// Variant index -> access type: 0 16B (16-aligned), 1 16B (8-aligned), 2 8B, 3 4B, 4 1B.
-template <int VAR> struct Vec;
-template <> struct Vec<0> { typedef u32x4a16 T; static constexpr int N = 16; };
-template <> struct Vec<1> { typedef u32x4a8 T;  static constexpr int N = 16; };
-template <> struct Vec<2> { typedef uint64_t T; static constexpr int N = 8; };
-template <> struct Vec<3> { typedef uint32_t T; static constexpr int N = 4; };
-template <> struct Vec<4> { typedef uint8_t T;  static constexpr int N = 1; };
+// Flat mapping: every lane owns one VS-byte unit (g, q) of one group and issues all k of
+// its loads back to back, so a wave keeps k * 64 * VS bytes in flight in a single phase.
+// The last unit of a block is shifted back to end at bb (loads stay inside the block) and
+// stores only the bytes no other unit owns, so no byte is written twice and an in-place
+// decode never reads a byte another lane has already rewritten and then uses it.
+//   encode: out = parity + g*out_gstride
+//   decode: out = blocks' slot eidx[g] (the slot tagged row >= k); the XOR runs over all
+//           k slots — the erased slot's own parity included (cauchy_256.cpp:505-531) —
+//           so the loads never wait on eidx, only the store does.
+typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
 
-// parity[g] = XOR_x data[g][x]; one wave per group.
-template <int VAR, int K>
-__global__ __launch_bounds__(256) void xor_encode_kernel(const uint8_t* __restrict__ data,
-                                                         uint8_t* __restrict__ parity, int k,
-                                                         int bb, long long groups,
-                                                         long long ostride) {
-    const int lane = threadIdx.x & 63;
-    const long long g = (long long)blockIdx.x * 4 + wave_id();
-    if (g >= groups) return;
-    typedef typename Vec<VAR>::T V;
-    const int kk = K ? K : k;
-    constexpr int VS = Vec<VAR>::N;
-    const int nq = bb / VS;
-    const uint8_t* src = data + g * (long long)kk * bb;
-    uint8_t* dst = parity + g * ostride;
-    for (int q = lane; q < nq; q += 64) {
-        const uint8_t* p = src + q * VS;
-        V acc = *(const V*)p;
-        if (K) {
-#pragma unroll
-            for (int x = 1; x < (K ? K : 1); ++x) acc ^= *(const V*)(p + (long long)x * bb);
-        } else {
-            for (int x = 1; x < kk; ++x) acc ^= *(const V*)(p + (long long)x * bb);
-        }
-        *(V*)(dst + q * VS) = acc;
+template <int VS> struct Unit;
+// Loads and stores are non-temporal: every byte is touched exactly once, and on gfx950
+// nt streaming measured +17-23% over the default policy with cold caches
+// (tools/microbench).
+template <> struct Unit<16> {
+    typedef u32x4a8 T;
+    static __device__ __forceinline__ T ld(const uint8_t* p) {
+        return __builtin_nontemporal_load((const T*)p);
     }
-    for (int i = nq * VS + lane; i < bb; i += 64) {   // tail bytes
-        uint8_t acc = src[i];
-        for (int x = 1; x < kk; ++x) acc ^= src[(long long)x * bb + i];
-        dst[i] = acc;
+    static __device__ __forceinline__ void st(uint8_t* p, T v) {
+        __builtin_nontemporal_store(v, (T*)p);
+    }
+};
+template <> struct Unit<4> {
+    typedef uint32_t T;
+    static __device__ __forceinline__ T ld(const uint8_t* p) {
+        return __builtin_nontemporal_load((const u32ua*)p);
+    }
+    static __device__ __forceinline__ void st(uint8_t* p, T v) {
+        __builtin_nontemporal_store(v, (u32ua*)p);
+    }
+};
+
+template <int VS, int K, bool DECODE>
+__global__ __launch_bounds__(256) void xor_flat_kernel(
+    const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ eidx, int k,
+    int bb, int nu, unsigned total_units, long long in_gstride, long long out_gstride) {
+    typedef typename Unit<VS>::T V;
+    const unsigned u = blockIdx.x * 256u + threadIdx.x;
+    if (u >= total_units) return;
+    const unsigned g = u / (unsigned)nu;
+    const int q = (int)(u - g * (unsigned)nu);
+    const int off = min(q * VS, bb - VS);
+    const uint8_t* p = in + (long long)g * in_gstride + off;
+    int e = 0;
+    if (DECODE) e = eidx[g];   // issued beside the data loads
+    V acc = Unit<VS>::ld(p);
+    if (K) {
+#pragma unroll
+        for (int x = 1; x < (K ? K : 1); ++x) acc ^= Unit<VS>::ld(p + (long long)x * bb);
+    } else {
+#pragma unroll 4
+        for (int x = 1; x < k; ++x) acc ^= Unit<VS>::ld(p + (long long)x * bb);
+    }
+    uint8_t* dst = out + (long long)g * out_gstride;
+    if (DECODE) {
+        if (e == 255) return;   // nothing erased in this group
+        dst += (long long)e * bb;
+    }
+    const int own = q * VS;   // first byte this unit owns
+    if (own + VS <= bb) {
+        Unit<VS>::st(dst + off, acc);
+    } else {
+        // tail unit: owns bytes [own, bb) = the top (bb - own) bytes of the shifted vector
+        const int skip = own - off;
+        const uint8_t* b = (const uint8_t*)&acc;
+        if (VS == 16 && skip == 8) {
+            *(uint64_t*)(dst + own) = ((const uint64_t*)b)[1];
+        } else {
+            for (int i = skip; i < VS; ++i) dst[off + i] = b[i];
+        }
     }
 }
 
-// m = 1 decode (cauchy_decode_m1, cauchy_256.cpp:486-540): the first slot with row >= k is
-// the erased slot e; out[e] = XOR of all k slots (its own parity included); its row becomes
-// the first data row not tagged by another slot.  One wave per group.
-template <int VAR>
-__global__ __launch_bounds__(256) void xor_decode_kernel(
-    const uint8_t* __restrict__ blocks, uint8_t* out, const uint8_t* __restrict__ rows_in,
-    uint8_t* rows_out, int32_t* __restrict__ status, int k, int bb, long long groups) {
-    __shared__ uint8_t seen[4][256];
-    const int lane = threadIdx.x & 63;
-    const int w = wave_id();
-    const long long g = (long long)blockIdx.x * 4 + w;
+// LDS-DMA variant (the shipped m = 1 path when a group is 16-byte aligned and fits):
+// each wave owns groups g = w, w + W, ... and streams a whole group (k*bb contiguous
+// bytes) into one of two LDS slots with global_load_lds_dwordx4 nt (1 KiB per wave
+// instruction), XORs the k blocks from LDS while the next group's DMA is in flight, and
+// writes 8-byte nt stores.  Measured 6.15 TB/s cold on the (10, 1, 1352) layout vs
+// 4.5 TB/s for plain loads (tools/microbench/dma_variants.hip).  The whole group is in
+// LDS before any byte is written, so an in-place decode has no read/write hazard.
+#define QF_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define QF_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits on gfx9");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr int kDmaWaves = 4;     // waves per workgroup (one per SIMD)
+constexpr int kDmaMaxKiB = 20;   // 4 waves x 2 slots x 20 KiB = 160 KiB of LDS
+
+template <int NDMA, bool DECODE>
+__global__ __launch_bounds__(kDmaWaves * 64) void xor_dma_kernel(
+    const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ eidx, int k,
+    int bb, long long groups, long long out_gstride) {
+    constexpr int SLOT = NDMA * 1024;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int w = wave_id(), lane = threadIdx.x & 63;
+    uint8_t* myl = smem + (size_t)w * 2 * SLOT;
+    const long long W = (long long)gridDim.x * kDmaWaves;
+    long long g = (long long)blockIdx.x * kDmaWaves + w;
+    if (g >= groups) return;
+    const int gb = k * bb;
+    auto issue = [&](long long gg, int slot) {
+        const uint8_t* src = in + gg * gb;
+#pragma unroll
+        for (int i = 0; i < NDMA; ++i) {
+            const int off = min(i * 1024 + lane * 16, gb - 16);   // last piece: clamp inside
+            __builtin_amdgcn_global_load_lds(QF_GPTR(src + off),
+                                             QF_LPTR(myl + slot * SLOT + i * 1024), 16, 0, 2);
+        }
+    };
+    // the erased-slot index of the next group is fetched before that group's DMA is
+    // issued, so the counted wait below also covers it (scalar or vector load alike)
+    int e_next = DECODE ? eidx[g] : 0;
+    issue(g, 0);
+    int slot = 0;
+    const int nq = bb >> 3;
+    for (; g < groups; g += W) {
+        const long long gn = g + W;
+        const int e = e_next;
+        if (gn < groups) {
+            if (DECODE) e_next = eidx[gn];
+            issue(gn, slot ^ 1);
+            wait_vmcnt<NDMA>();   // group g landed (the NDMA younger ops are group gn)
+        } else {
+            wait_vmcnt<0>();
+        }
+        if (!DECODE || e != 255) {
+            const uint8_t* L = myl + slot * SLOT;
+            uint8_t* o = out + g * out_gstride + (long long)e * bb;
+            for (int q = lane; q < nq; q += 64) {
+                uint64_t acc = *(const uint64_t*)(L + q * 8);
+                int x = 1;
+                for (; x + 1 < k; x += 2)
+                    acc ^= *(const uint64_t*)(L + x * bb + q * 8) ^
+                           *(const uint64_t*)(L + (x + 1) * bb + q * 8);
+                if (x < k) acc ^= *(const uint64_t*)(L + x * bb + q * 8);
+                __builtin_nontemporal_store(acc, (uint64_t*)(o + q * 8));
+            }
+        }
+        slot ^= 1;
+    }
+}
+
+// Tiny blocks (bb < 4): one byte per lane.
+template <bool DECODE>
+__global__ __launch_bounds__(256) void xor_bytes_kernel(
+    const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ eidx, int k,
+    int bb, long long total, long long in_gstride, long long out_gstride) {
+    const long long u = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (u >= total) return;
+    const long long g = u / bb;
+    const int i = (int)(u % bb);
+    const uint8_t* p = in + g * in_gstride + i;
+    uint8_t acc = 0;
+    for (int x = 0; x < k; ++x) acc ^= p[(long long)x * bb];
+    uint8_t* dst = out + g * out_gstride;
+    if (DECODE) {
+        const int e = eidx[g];
+        if (e == 255) return;
+        dst += (long long)e * bb;
+    }
+    dst[i] = acc;
+}
+
+// m = 1 decode bookkeeping (cauchy_decode_m1, cauchy_256.cpp:486-540), one thread per
+// group: the erased slot is the first with row >= k; its new row is the first data row
+// not tagged by any other slot.  eidx[g] = that slot (255 = nothing erased).
+__global__ __launch_bounds__(256) void m1_prep_kernel(const uint8_t* __restrict__ rows_in,
+                                                      uint8_t* rows_out,
+                                                      int32_t* __restrict__ status,
+                                                      uint8_t* __restrict__ eidx, int k,
+                                                      long long groups) {
+    const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
     if (g >= groups) return;
     const uint8_t* rg = rows_in + g * k;
-    uint8_t* sw = seen[w];
-    for (int i = lane; i < 256; i += 64) sw[i] = 0;
-    __builtin_amdgcn_wave_barrier();
-    int e = -1;
-    for (int base = 0; base < k && e < 0; base += 64) {
-        const int i = base + lane;
-        const bool er = i < k && rg[i] >= k;
-        const unsigned long long msk = __ballot(er);
-        if (msk) e = base + __ffsll((long long)msk) - 1;
-    }
-    e = __builtin_amdgcn_readfirstlane(e);
-    if (status && lane == 0) status[g] = 0;
     uint8_t* ro = rows_out + g * k;
-    if (ro != rg)
-        for (int i = lane; i < k; i += 64) ro[i] = rg[i];
-    if (e < 0) return;   // nothing erased
-    for (int i = lane; i < k; i += 64)
-        if (i != e && rg[i] < k) sw[rg[i]] = 1;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    uint64_t seen[4] = {0, 0, 0, 0};
+    int e = -1;
+    for (int i = 0; i < k; ++i) {
+        const int r = rg[i];
+        if (r >= k) {
+            if (e < 0) { e = i; continue; }
+        }
+        if (r < k) seen[r >> 6] |= 1ull << (r & 63);
+        if (ro != rg) ro[i] = (uint8_t)r;
+    }
+    if (status) status[g] = 0;
+    if (e < 0) {
+        eidx[g] = 255;
+        return;
+    }
     int miss = -1;
-    for (int base = 0; base < k && miss < 0; base += 64) {
-        const int x = base + lane;
-        const unsigned long long msk = __ballot(x < k && !sw[x]);
-        if (msk) miss = base + __ffsll((long long)msk) - 1;
+    for (int w = 0; w < 4 && miss < 0; ++w) {
+        const uint64_t free = ~seen[w];
+        if (free) {
+            const int b = w * 64 + __ffsll((long long)free) - 1;
+            if (b < k) miss = b;
+            break;
+        }
     }
-    const uint8_t* src = blocks + g * (long long)k * bb;
-    uint8_t* dst = out + g * (long long)k * bb + (long long)e * bb;
-    typedef typename Vec<VAR>::T V;
-    constexpr int VS = Vec<VAR>::N;
-    const int nq = bb / VS;
-    for (int q = lane; q < nq; q += 64) {
-        const uint8_t* p = src + q * VS;
-        V acc = *(const V*)(p + (long long)e * bb);
-        for (int x = 0; x < k; ++x)
-            if (x != e) acc ^= *(const V*)(p + (long long)x * bb);
-        *(V*)(dst + q * VS) = acc;
-    }
-    for (int i = nq * VS + lane; i < bb; i += 64) {
-        uint8_t acc = src[(long long)e * bb + i];
-        for (int x = 0; x < k; ++x)
-            if (x != e) acc ^= src[(long long)x * bb + i];
-        dst[i] = acc;
-    }
-    if (lane == 0 && miss >= 0) ro[e] = (uint8_t)miss;
+    ro[e] = miss >= 0 ? (uint8_t)miss : rg[e];
+    eidx[g] = (uint8_t)e;
 }
 
 __global__ void replicate_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ parity,
@@ -335,6 +439,141 @@ __global__ __launch_bounds__(256) void gf_apply_kernel(
             const int o = chunk * RC + j;
             const int slot = (DECODE && slots) ? slots[(long long)g * rmax + o] : o;
             uint8_t* dst = out + (long long)g * out_gstride + (long long)slot * bb;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) store_word(dst + r * s, c, ca, acc[j][r]);
+        }
+    }
+}
+
+// LDS-staged variant (shipped for m > 1 whenever a group is 16-byte aligned): one
+// workgroup per group; waves = column tiles x output chunks, all reading the same staged
+// blocks.  Wave 0 streams block x + NSLOT - 1 into a ring of NSLOT block slots with
+// global_load_lds_dwordx4 nt (the DMA window starts at the 16-byte boundary at or below
+// the block, so no lane straddles the group end), and one workgroup barrier per block
+// both publishes the landed block and frees the slot of block x - 1.  The block's
+// sub-row words are read from LDS with unaligned ds_read_b32.  Every global read of the
+// group completes before any output is stored, so in-place decode needs no staging
+// copy even when the outputs span several chunks.
+__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
+    switch (n) {
+#define QF_W(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+        QF_W(0) QF_W(1) QF_W(2) QF_W(3) QF_W(4) QF_W(5) QF_W(6) QF_W(7) QF_W(8) QF_W(9)
+        QF_W(10) QF_W(11) QF_W(12) QF_W(13) QF_W(14) QF_W(15) QF_W(16) QF_W(17) QF_W(18)
+        QF_W(19) QF_W(20) QF_W(21) QF_W(22) QF_W(23) QF_W(24) QF_W(25) QF_W(26) QF_W(27)
+        QF_W(28) QF_W(29) QF_W(30) QF_W(31) QF_W(32) QF_W(33) QF_W(34) QF_W(35) QF_W(36)
+#undef QF_W
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+constexpr int kStageSlots = 4;   // ring depth: 3 blocks in flight while one is combined
+
+// Workgroup-size bound per output-chunk width: it caps VGPRs at 512 / ceil(waves / 4), so
+// the RC x 8 accumulators never spill (RC 4: 128 VGPR, RC 8: 170, RC 16: 256).
+template <int RC> struct StageBound { static constexpr int T = RC <= 4 ? 1024 : (RC == 8 ? 640 : 320); };
+
+template <int RC, bool DECODE>
+__global__ __launch_bounds__(StageBound<RC>::T) void gf_stage_kernel(
+    const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ coef,
+    const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, int k, int m, int bb,
+    int nw, int ntiles, int nchunk, int rmax, int npc, long long coef_gstride,
+    long long out_gstride) {
+    constexpr int RCP = RC < 4 ? 4 : RC;
+    constexpr int NCW = RCP / 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63;
+    const int w = wave_id();
+    const int nwaves = ntiles * nchunk;
+    const int tile = w % ntiles;
+    const int chunk = w / ntiles;
+    const long long g = blockIdx.x;
+    const int s = bb >> 3;
+    const int SB = npc * 1024;
+    const long long gb = (long long)k * bb;
+    const uint8_t* gin = in + g * gb;
+    int n = DECODE ? nout[g] : m;
+    n = min(n - chunk * RC, RC);
+    const int c = tile * 64 + lane;
+    const ColAccess ca = col_access<false>(c, nw, s);
+    if (DECODE && __builtin_amdgcn_readfirstlane(nout[g]) == 0) return;   // whole group idle
+
+    // This group's coefficient table ([nchunk][k][RCP] bytes) goes to LDS once, so the
+    // per-block coefficient fetch is an LDS broadcast, not a dependent global load.
+    uint32_t* lcoef = (uint32_t*)(smem + kStageSlots * SB);
+    {
+        const uint32_t* src = (const uint32_t*)(coef + g * coef_gstride);
+        const int nwords = nchunk * k * NCW;
+        for (int i = threadIdx.x; i < nwords; i += blockDim.x) lcoef[i] = src[i];
+    }
+
+    // DMA of block x: the 16-byte-aligned window [a0, a1) around the block, npc pieces of
+    // 1 KiB.  Lanes past a1 are masked; lane 0 always stays active (clamped into the
+    // window) so every piece is issued and the vmcnt arithmetic stays exact.
+    auto issue = [&](int x) {
+        const long long a0 = ((long long)x * bb) & ~15ll;
+        const long long a1 = (((long long)(x + 1) * bb) + 15) & ~15ll;
+        uint8_t* dst = smem + (x % kStageSlots) * SB;
+        for (int p = 0; p < npc; ++p) {
+            long long off = a0 + p * 1024 + lane * 16;
+            const bool act = off < a1;
+            if (!act) off = a1 - 16;
+            if (act || lane == 0)
+                __builtin_amdgcn_global_load_lds(QF_GPTR(gin + off), QF_LPTR(dst + p * 1024), 16,
+                                                 0, 2);
+        }
+    };
+    __syncthreads();   // lcoef visible (its fence drains only the coefficient loads)
+    constexpr int A = kStageSlots - 1;
+    if (w == 0)
+        for (int x = 0; x < A && x < k; ++x) issue(x);
+
+    uint32_t acc[RC][8];
+#pragma unroll
+    for (int j = 0; j < RC; ++j)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc[j][r] = 0;
+
+#pragma unroll 1
+    for (int x = 0; x < k; ++x) {
+        if (w == 0) {
+            const int issued = min(k, x + A);
+            wait_vmcnt_dyn(issued - x - 1 == A - 1 ? (A - 1) * npc : 0);
+        }
+        if (nwaves > 1) {
+            // raw barrier: __syncthreads() would emit vmcnt(0) and drain the DMA pipeline.
+            // Wave 0's counted wait above retired block x; the barrier publishes it to the
+            // other waves and proves block x - 1's slot is no longer being read.
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+        if (w == 0 && x + A < k) issue(x + A);
+        if (n > 0) {
+            uint32_t cwv[NCW];
+#pragma unroll
+            for (int q = 0; q < NCW; ++q)
+                cwv[q] = __builtin_amdgcn_readfirstlane(lcoef[(chunk * k + x) * NCW + q]);
+            const uint8_t* blk = smem + (x % kStageSlots) * SB + (((long long)x * bb) & 15) + ca.lo;
+            WZ v;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v.W[t] = (*(const u32ua*)(blk + t * s)) >> ca.shift;
+            expand_wz(v);
+#pragma unroll
+            for (int j = 0; j < RC; ++j) {
+                if (j < n) {
+                    const uint32_t a = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                    apply_nibble<0>(acc[j], a & 15u, v);
+                    apply_nibble<4>(acc[j], a >> 4, v);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < RC; ++j) {
+        if (j < n) {
+            const int o = chunk * RC + j;
+            const int slot = (DECODE && slots) ? slots[g * rmax + o] : o;
+            uint8_t* dst = out + g * out_gstride + (long long)slot * bb;
 #pragma unroll
             for (int r = 0; r < 8; ++r) store_word(dst + r * s, c, ca, acc[j][r]);
         }
@@ -557,61 +796,100 @@ __global__ __launch_bounds__(256) void synth_gather_kernel(
 // ---------------------------------------------------------------------- launchers
 static inline unsigned blocks_for_waves(long long waves) { return (unsigned)((waves + 3) / 4); }
 
-static int xor_variant(const void* a, const void* b, int bb) {
-    // 0: 16B aligned-16, 1: 16B aligned-8, 2: 8B, 3: 4B, 4: 1B
-    const uintptr_t al = (uintptr_t)a | (uintptr_t)b | (uintptr_t)bb;
-    static int forced = -2;
-    if (forced == -2) {
-        const char* e = getenv("QFEC_XOR_VARIANT");
-        forced = e ? atoi(e) : -1;
-    }
-    int v;
-    if ((al & 15) == 0) v = 0;
-    else if ((al & 7) == 0) v = 1;
-    else if ((al & 3) == 0) v = 3;
-    else v = 4;
-    if (forced >= 0 && forced >= v) v = forced;   // may only relax alignment
-    return v;
+// 16-byte units need 8-byte alignment of both buffers and of every block; otherwise
+// unaligned 4-byte units; blocks under 4 bytes go bytewise.
+static int xor_unit(const void* a, const void* b, long long s1, long long s2, int bb) {
+    const uintptr_t al = (uintptr_t)a | (uintptr_t)b | (uintptr_t)s1 | (uintptr_t)s2 |
+                         (uintptr_t)bb;
+    if (bb >= 16 && (al & 7) == 0) return 16;
+    return bb >= 4 ? 4 : 1;
 }
 
-template <int V>
-static void xor_encode_dispatch(const uint8_t* d, uint8_t* p, int k, int bb, long long G,
-                                long long os, hipStream_t st) {
-    const unsigned nb = blocks_for_waves(G);
+template <int VS, bool DECODE>
+static void xor_flat_launch(const uint8_t* in, uint8_t* out, const uint8_t* eidx, int k, int bb,
+                            long long G, long long igs, long long ogs, hipStream_t st) {
+    const int nu = (bb + VS - 1) / VS;
+    const unsigned total = (unsigned)(G * nu);
+    const unsigned nb = (total + 255) / 256;
     switch (k) {
-        case 10: xor_encode_kernel<V, 10><<<nb, 256, 0, st>>>(d, p, k, bb, G, os); break;
-        case 5: xor_encode_kernel<V, 5><<<nb, 256, 0, st>>>(d, p, k, bb, G, os); break;
-        case 32: xor_encode_kernel<V, 32><<<nb, 256, 0, st>>>(d, p, k, bb, G, os); break;
-        default: xor_encode_kernel<V, 0><<<nb, 256, 0, st>>>(d, p, k, bb, G, os); break;
+        case 10: xor_flat_kernel<VS, 10, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs); break;
+        case 32: xor_flat_kernel<VS, 32, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs); break;
+        default: xor_flat_kernel<VS, 0, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs); break;
     }
+}
+
+static int num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+template <bool DECODE, int N>
+static void xor_dma_launch_n(int ndma, const uint8_t* in, uint8_t* out, const uint8_t* eidx,
+                             int k, int bb, long long G, long long ogs, hipStream_t st) {
+    if constexpr (N > kDmaMaxKiB) {
+        return;
+    } else {
+        if (ndma != N) return xor_dma_launch_n<DECODE, N + 1>(ndma, in, out, eidx, k, bb, G, ogs, st);
+        const size_t lds = (size_t)kDmaWaves * 2 * N * 1024;
+        const long long want = (G + kDmaWaves - 1) / kDmaWaves;
+        const unsigned nb = (unsigned)std::min<long long>(want, (long long)num_cus());
+        xor_dma_kernel<N, DECODE><<<nb, kDmaWaves * 64, lds, st>>>(in, out, eidx, k, bb, G, ogs);
+    }
+}
+
+static bool xor_dma_ok(const void* in, const void* out, int k, int bb, long long ogs) {
+    static int disabled = -1;
+    if (disabled < 0) {
+        const char* e = getenv("QFEC_NO_DMA");
+        disabled = e && atoi(e) ? 1 : 0;
+    }
+    const long long gb = (long long)k * bb;
+    return !disabled && bb % 8 == 0 && gb % 16 == 0 && gb >= 16 &&
+           ((uintptr_t)in & 15) == 0 && (((uintptr_t)out | (uintptr_t)ogs) & 7) == 0 &&
+           (gb + 1023) / 1024 <= kDmaMaxKiB;
+}
+
+template <bool DECODE>
+static hipError_t xor_any(const uint8_t* in, uint8_t* out, const uint8_t* eidx, int k, int bb,
+                          long long G, long long igs, long long ogs, hipStream_t st) {
+    if (G <= 0) return hipSuccess;
+    if (igs == (long long)k * bb && xor_dma_ok(in, out, k, bb, ogs)) {
+        const int ndma = (int)((igs + 1023) / 1024);
+        xor_dma_launch_n<DECODE, 1>(ndma, in, out, eidx, k, bb, G, ogs, st);
+        return hipGetLastError();
+    }
+    const int vs = xor_unit(in, out, igs, ogs, bb);
+    const long long units = G * ((bb + vs - 1) / vs);
+    if (units > 0xffffffffLL) return hipErrorInvalidValue;
+    if (vs == 16) xor_flat_launch<16, DECODE>(in, out, eidx, k, bb, G, igs, ogs, st);
+    else if (vs == 4) xor_flat_launch<4, DECODE>(in, out, eidx, k, bb, G, igs, ogs, st);
+    else xor_bytes_kernel<DECODE><<<(unsigned)((units + 255) / 256), 256, 0, st>>>(in, out, eidx, k, bb, units, igs, ogs);
+    return hipGetLastError();
 }
 
 hipError_t launch_xor_encode(const uint8_t* data, uint8_t* parity, int k, int bb,
                              long long groups, long long out_gstride, hipStream_t st) {
-    if (groups <= 0) return hipSuccess;
-    switch (xor_variant(data, parity, (int)(bb | out_gstride))) {
-        case 0: xor_encode_dispatch<0>(data, parity, k, bb, groups, out_gstride, st); break;
-        case 1: xor_encode_dispatch<1>(data, parity, k, bb, groups, out_gstride, st); break;
-        case 2: xor_encode_dispatch<2>(data, parity, k, bb, groups, out_gstride, st); break;
-        case 3: xor_encode_dispatch<3>(data, parity, k, bb, groups, out_gstride, st); break;
-        default: xor_encode_dispatch<4>(data, parity, k, bb, groups, out_gstride, st); break;
-    }
-    return hipGetLastError();
+    return xor_any<false>(data, parity, nullptr, k, bb, groups, (long long)k * bb, out_gstride,
+                          st);
 }
 
 hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t* rows_in,
-                             uint8_t* rows_out, int32_t* status, int k, int bb,
+                             uint8_t* rows_out, int32_t* status, uint8_t* eidx, int k, int bb,
                              long long groups, hipStream_t st) {
     if (groups <= 0) return hipSuccess;
-    const unsigned nb = blocks_for_waves(groups);
-    switch (xor_variant(blocks, out, bb)) {
-        case 0: xor_decode_kernel<0><<<nb, 256, 0, st>>>(blocks, out, rows_in, rows_out, status, k, bb, groups); break;
-        case 1: xor_decode_kernel<1><<<nb, 256, 0, st>>>(blocks, out, rows_in, rows_out, status, k, bb, groups); break;
-        case 2: xor_decode_kernel<2><<<nb, 256, 0, st>>>(blocks, out, rows_in, rows_out, status, k, bb, groups); break;
-        case 3: xor_decode_kernel<3><<<nb, 256, 0, st>>>(blocks, out, rows_in, rows_out, status, k, bb, groups); break;
-        default: xor_decode_kernel<4><<<nb, 256, 0, st>>>(blocks, out, rows_in, rows_out, status, k, bb, groups); break;
-    }
-    return hipGetLastError();
+    m1_prep_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(rows_in, rows_out, status,
+                                                                     eidx, k, groups);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return xor_any<true>(blocks, out, eidx, k, bb, groups, (long long)k * bb, (long long)k * bb,
+                         st);
 }
 
 hipError_t launch_replicate(const uint8_t* data, uint8_t* parity, int m, int bb,
@@ -631,6 +909,15 @@ hipError_t launch_rows_k1(const uint8_t* rows_in, uint8_t* rows_out, int32_t* st
     return hipGetLastError();
 }
 
+static bool stage_disabled() {
+    static int d = -1;
+    if (d < 0) {
+        const char* e = getenv("QFEC_NO_STAGE");
+        d = e && atoi(e) ? 1 : 0;
+    }
+    return d;
+}
+
 template <bool DECODE>
 static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8_t* coef,
                                     const uint8_t* slots, const int32_t* nout, int k, int m,
@@ -643,6 +930,30 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
     const long long units = groups * nchunk * ntiles;
     if (units <= 0) return hipSuccess;
     if (units > 0x7fffffffLL) return hipErrorInvalidValue;
+    const long long gb = (long long)k * bb;
+    const int npc = (int)((15 + bb + 1023) / 1024);
+    const int rcp = rc < 4 ? 4 : rc;
+    // ring of block slots + this group's coefficient table
+    const size_t lds = (size_t)kStageSlots * npc * 1024 + (((size_t)nchunk * k * rcp + 15) & ~15ull);
+    const int maxt = rc <= 4 ? 1024 : (rc == 8 ? 640 : 320);
+    if (!stage_disabled() && s >= 4 && gb % 16 == 0 && ((uintptr_t)in & 15) == 0 &&
+        ntiles * nchunk * 64 <= maxt && lds <= 64 * 1024 && groups <= 0x7fffffffLL) {
+        const unsigned nthreads = (unsigned)(ntiles * nchunk * 64);
+#define QF_STAGE(RCV)                                                                         \
+    gf_stage_kernel<RCV, DECODE><<<(unsigned)groups, nthreads, lds, st>>>(                    \
+        in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, npc, coef_gstride,    \
+        out_gstride)
+        switch (rc) {
+            case 1: QF_STAGE(1); break;
+            case 2: QF_STAGE(2); break;
+            case 4: QF_STAGE(4); break;
+            case 8: QF_STAGE(8); break;
+            case 16: QF_STAGE(16); break;
+            default: return hipErrorInvalidValue;
+        }
+#undef QF_STAGE
+        return hipGetLastError();
+    }
     const unsigned nb = blocks_for_waves(units);
     const int tu = (int)units;
 #define QF_LAUNCH(RCV)                                                                        \
@@ -666,6 +977,21 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
     }
 #undef QF_LAUNCH
     return hipGetLastError();
+}
+
+// True when gf_apply_dispatch will take the staged path (in-place decode then needs no
+// scratch even with several output chunks).
+bool gf_staged(const void* in, int k, int bb, int nchunk, int rc) {
+    const int s = bb / 8;
+    const int nw = (s + 3) / 4;
+    const int ntiles = (nw + 63) / 64;
+    const long long gb = (long long)k * bb;
+    const int npc = (int)((15 + bb + 1023) / 1024);
+    const int maxt = rc <= 4 ? 1024 : (rc == 8 ? 640 : 320);
+    const size_t lds = (size_t)kStageSlots * npc * 1024 +
+                       (((size_t)nchunk * k * (rc < 4 ? 4 : rc) + 15) & ~15ull);
+    return !stage_disabled() && s >= 4 && gb % 16 == 0 && ((uintptr_t)in & 15) == 0 &&
+           ntiles * nchunk * 64 <= maxt && lds <= 64 * 1024;
 }
 
 hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t* coef, int k,
