@@ -14,9 +14,10 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
             -mllvm -structurizecfg-skip-uniform-regions=true \
             -DQFEC_BUILD -DQFEC_TABLES_PATH='"$(TABLES)"' -Wall -Wno-unused-function
 
-SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/fec_api.cpp
-HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(ROOT)include/quic_fec.h $(ROOT)Makefile
-OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/fec_api.o
+SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp
+HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(ROOT)include/quic_fec.h \
+        $(ROOT)include/quic_fec_group.h $(ROOT)Makefile
+OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o
 
 .PHONY: all lib oracle clean
 all: lib oracle
@@ -28,6 +29,10 @@ $(ROOT)build/fec_kernels.o: $(CSRC)/fec_kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(ROOT)build/fec_api.o: $(CSRC)/fec_api.cpp $(HDRS) $(TABLES)
+	@mkdir -p $(ROOT)build
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(ROOT)build/fec_group.o: $(CSRC)/fec_group.cpp $(HDRS)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 

@@ -135,18 +135,44 @@ __device__ __forceinline__ void wait_vmcnt() {
 constexpr int kDmaWaves = 4;     // waves per workgroup (one per SIMD)
 constexpr int kDmaMaxKiB = 20;   // 4 waves x 2 slots x 20 KiB = 160 KiB of LDS
 
+// m = 1 decode bookkeeping for one group, done by the wave that decodes it (k <= 64,
+// one row tag per lane; cauchy_decode_m1, cauchy_256.cpp:486-540).  `r` is this lane's
+// row tag (lanes >= k hold 255).  Returns the erased slot (-1 if none) and writes
+// rows_out / status.
+__device__ __forceinline__ int m1_rows_wave(int r, int k, uint8_t* flags, uint8_t* ro,
+                                            int32_t* status, long long g) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long er = __ballot(lane < k && r >= k);
+    const int e = er ? __ffsll((long long)er) - 1 : -1;
+    flags[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < k && lane != e && r < k) flags[r] = 1;
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long miss = __ballot(lane < k && !flags[lane]);
+    if (lane < k) {
+        int v = r;
+        if (lane == e && miss) v = __ffsll((long long)miss) - 1;
+        ro[lane] = (uint8_t)v;
+    }
+    if (status && lane == 0) status[g] = 0;
+    return e;
+}
+
 template <int NDMA, bool DECODE>
 __global__ __launch_bounds__(kDmaWaves * 64) void xor_dma_kernel(
-    const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ eidx, int k,
-    int bb, long long groups, long long out_gstride) {
+    const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ eidx,
+    const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
+    int k, int bb, long long groups, long long out_gstride) {
     constexpr int SLOT = NDMA * 1024;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int w = wave_id(), lane = threadIdx.x & 63;
     uint8_t* myl = smem + (size_t)w * 2 * SLOT;
+    uint8_t* flags = smem + (size_t)kDmaWaves * 2 * SLOT + w * 64;
     const long long W = (long long)gridDim.x * kDmaWaves;
     long long g = (long long)blockIdx.x * kDmaWaves + w;
     if (g >= groups) return;
     const int gb = k * bb;
+    const bool fused = DECODE && rows_in != nullptr;   // rows handled here (k <= 64)
     auto issue = [&](long long gg, int slot) {
         const uint8_t* src = in + gg * gb;
 #pragma unroll
@@ -156,23 +182,33 @@ __global__ __launch_bounds__(kDmaWaves * 64) void xor_dma_kernel(
                                              QF_LPTR(myl + slot * SLOT + i * 1024), 16, 0, 2);
         }
     };
-    // the erased-slot index of the next group is fetched before that group's DMA is
-    // issued, so the counted wait below also covers it (scalar or vector load alike)
-    int e_next = DECODE ? eidx[g] : 0;
+    // The next group's row tags (or erased-slot index) are fetched before that group's
+    // DMA is issued, so the counted wait below also covers them.
+    auto fetch_rows = [&](long long gg) -> int {
+        if (!DECODE) return 0;
+        if (fused) return lane < k ? rows_in[gg * k + lane] : 255;
+        return eidx[gg];
+    };
+    int r_next = fetch_rows(g);
     issue(g, 0);
     int slot = 0;
     const int nq = bb >> 3;
     for (; g < groups; g += W) {
         const long long gn = g + W;
-        const int e = e_next;
+        const int r_cur = r_next;
         if (gn < groups) {
-            if (DECODE) e_next = eidx[gn];
+            r_next = fetch_rows(gn);
             issue(gn, slot ^ 1);
             wait_vmcnt<NDMA>();   // group g landed (the NDMA younger ops are group gn)
         } else {
             wait_vmcnt<0>();
         }
-        if (!DECODE || e != 255) {
+        int e = 0;
+        if (DECODE) {
+            e = fused ? m1_rows_wave(r_cur, k, flags, rows_out + g * k, status, g) : r_cur;
+            if (!fused && e == 255) e = -1;
+        }
+        if (!DECODE || e >= 0) {
             const uint8_t* L = myl + slot * SLOT;
             uint8_t* o = out + g * out_gstride + (long long)e * bb;
             for (int q = lane; q < nq; q += 64) {
@@ -366,7 +402,7 @@ __device__ __forceinline__ void store_word(uint8_t* sub, int c, const ColAccess&
 //   coef:  [(g) * coef_gstride + (chunk * k + pos) * RCP + j]  (RCP = max(4, RC))
 //   encode: outputs o = chunk*RC + j < m go to out + g*out_gstride + o*bb
 //   decode: outputs o < nout[g] go to out + g*out_gstride + slots[g*rmax + o]*bb
-template <int RC, bool DECODE, bool TINY>
+template <int RC, bool DECODE, bool TINY, int PD>
 __global__ __launch_bounds__(256) void gf_apply_kernel(
     const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, int k, int m, int bb,
@@ -398,37 +434,42 @@ __global__ __launch_bounds__(256) void gf_apply_kernel(
 #pragma unroll
         for (int r = 0; r < 8; ++r) acc[j][r] = 0;
 
-    // Software pipeline: block pos+1's raw words and coefficients are in flight while
-    // block pos is combined (the realigning shift is applied at use, so the compiler's
-    // vmcnt wait lands in the next iteration).
-    uint32_t raw[8];
+    // Software pipeline PD blocks deep: raw words of blocks pos+1 .. pos+PD are in flight
+    // while block pos is combined (the realigning shift is applied at use, so the
+    // compiler's vmcnt wait lands at the consumer).  The loop is unrolled by PD so every
+    // ring slot is a fixed register set.  Loads past the last block are clamped to it.
+    uint32_t raw[PD][8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) raw[t] = load_raw<TINY>(gin + t * s, ca, s);
-    uint32_t cwn[NCW];
+    for (int u = 0; u < PD; ++u) {
+        const uint8_t* p = gin + (long long)min(u, k - 1) * bb;
 #pragma unroll
-    for (int q = 0; q < NCW; ++q) cwn[q] = cw[q];
+        for (int t = 0; t < 8; ++t) raw[u][t] = load_raw<TINY>(p + t * s, ca, s);
+    }
 
 #pragma unroll 1
-    for (int pos = 0; pos < k; ++pos) {
-        WZ v;
+    for (int pos0 = 0; pos0 < k; pos0 += PD) {
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v.W[t] = TINY ? raw[t] : (raw[t] >> ca.shift);
-        uint32_t cwv[NCW];
+        for (int u = 0; u < PD; ++u) {
+            const int pos = pos0 + u;
+            if (pos < k) {
+                WZ v;
 #pragma unroll
-        for (int q = 0; q < NCW; ++q) cwv[q] = cwn[q];
-        const int pn = pos + 1 < k ? pos + 1 : pos;   // clamped: no branch around the loads
-        const uint8_t* p = gin + (long long)pn * bb;
+                for (int t = 0; t < 8; ++t) v.W[t] = TINY ? raw[u][t] : (raw[u][t] >> ca.shift);
+                const uint8_t* p = gin + (long long)min(pos + PD, k - 1) * bb;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) raw[t] = load_raw<TINY>(p + t * s, ca, s);
+                for (int t = 0; t < 8; ++t) raw[u][t] = load_raw<TINY>(p + t * s, ca, s);
+                uint32_t cwv[NCW];
 #pragma unroll
-        for (int q = 0; q < NCW; ++q) cwn[q] = cw[pn * NCW + q];
-        expand_wz(v);
+                for (int q = 0; q < NCW; ++q) cwv[q] = cw[pos * NCW + q];
+                expand_wz(v);
 #pragma unroll
-        for (int j = 0; j < RC; ++j) {
-            if (j < n) {
-                const uint32_t a = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-                apply_nibble<0>(acc[j], a & 15u, v);
-                apply_nibble<4>(acc[j], a >> 4, v);
+                for (int j = 0; j < RC; ++j) {
+                    if (j < n) {
+                        const uint32_t a = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                        apply_nibble<0>(acc[j], a & 15u, v);
+                        apply_nibble<4>(acc[j], a >> 4, v);
+                    }
+                }
             }
         }
     }
@@ -830,17 +871,26 @@ static int num_cus() {
     return n;
 }
 
+struct RowsIO {
+    const uint8_t* rows_in;   // non-null: decode kernel does the m = 1 bookkeeping itself
+    uint8_t* rows_out;
+    int32_t* status;
+};
+
 template <bool DECODE, int N>
 static void xor_dma_launch_n(int ndma, const uint8_t* in, uint8_t* out, const uint8_t* eidx,
-                             int k, int bb, long long G, long long ogs, hipStream_t st) {
+                             RowsIO rio, int k, int bb, long long G, long long ogs,
+                             hipStream_t st) {
     if constexpr (N > kDmaMaxKiB) {
         return;
     } else {
-        if (ndma != N) return xor_dma_launch_n<DECODE, N + 1>(ndma, in, out, eidx, k, bb, G, ogs, st);
-        const size_t lds = (size_t)kDmaWaves * 2 * N * 1024;
+        if (ndma != N)
+            return xor_dma_launch_n<DECODE, N + 1>(ndma, in, out, eidx, rio, k, bb, G, ogs, st);
+        const size_t lds = (size_t)kDmaWaves * 2 * N * 1024 + kDmaWaves * 64;
         const long long want = (G + kDmaWaves - 1) / kDmaWaves;
         const unsigned nb = (unsigned)std::min<long long>(want, (long long)num_cus());
-        xor_dma_kernel<N, DECODE><<<nb, kDmaWaves * 64, lds, st>>>(in, out, eidx, k, bb, G, ogs);
+        xor_dma_kernel<N, DECODE><<<nb, kDmaWaves * 64, lds, st>>>(
+            in, out, eidx, rio.rows_in, rio.rows_out, rio.status, k, bb, G, ogs);
     }
 }
 
@@ -853,7 +903,7 @@ static bool xor_dma_ok(const void* in, const void* out, int k, int bb, long long
     const long long gb = (long long)k * bb;
     return !disabled && bb % 8 == 0 && gb % 16 == 0 && gb >= 16 &&
            ((uintptr_t)in & 15) == 0 && (((uintptr_t)out | (uintptr_t)ogs) & 7) == 0 &&
-           (gb + 1023) / 1024 <= kDmaMaxKiB;
+           (gb + 1023) / 1024 + 1 <= kDmaMaxKiB;
 }
 
 template <bool DECODE>
@@ -862,7 +912,8 @@ static hipError_t xor_any(const uint8_t* in, uint8_t* out, const uint8_t* eidx, 
     if (G <= 0) return hipSuccess;
     if (igs == (long long)k * bb && xor_dma_ok(in, out, k, bb, ogs)) {
         const int ndma = (int)((igs + 1023) / 1024);
-        xor_dma_launch_n<DECODE, 1>(ndma, in, out, eidx, k, bb, G, ogs, st);
+        xor_dma_launch_n<DECODE, 1>(ndma, in, out, eidx, RowsIO{nullptr, nullptr, nullptr}, k,
+                                    bb, G, ogs, st);
         return hipGetLastError();
     }
     const int vs = xor_unit(in, out, igs, ogs, bb);
@@ -884,6 +935,14 @@ hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t*
                              uint8_t* rows_out, int32_t* status, uint8_t* eidx, int k, int bb,
                              long long groups, hipStream_t st) {
     if (groups <= 0) return hipSuccess;
+    const long long gb = (long long)k * bb;
+    if (k <= 64 && xor_dma_ok(blocks, out, k, bb, gb)) {
+        // single launch: the DMA kernel also does the erased-slot / missing-row bookkeeping
+        const int ndma = (int)((gb + 1023) / 1024);
+        xor_dma_launch_n<true, 1>(ndma, blocks, out, nullptr, RowsIO{rows_in, rows_out, status},
+                                  k, bb, groups, gb, st);
+        return hipGetLastError();
+    }
     m1_prep_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(rows_in, rows_out, status,
                                                                      eidx, k, groups);
     hipError_t e = hipGetLastError();
@@ -907,6 +966,17 @@ hipError_t launch_rows_k1(const uint8_t* rows_in, uint8_t* rows_out, int32_t* st
     rows_k1_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(rows_in, rows_out, status,
                                                                      groups);
     return hipGetLastError();
+}
+
+// Register-pipeline depth of gf_apply_kernel (QFEC_PD=1|2|3 for experiments).
+static int pd_choice() {
+    static int pd = -1;
+    if (pd < 0) {
+        const char* e = getenv("QFEC_PD");
+        pd = e ? atoi(e) : 2;
+        if (pd < 1 || pd > 3) pd = 2;
+    }
+    return pd;
 }
 
 static bool stage_disabled() {
@@ -958,12 +1028,20 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
     const int tu = (int)units;
 #define QF_LAUNCH(RCV)                                                                        \
     do {                                                                                      \
-        if (s >= 4)                                                                           \
-            gf_apply_kernel<RCV, DECODE, false><<<nb, 256, 0, st>>>(                          \
+        if (s >= 4 && pd_choice() == 3)                                                       \
+            gf_apply_kernel<RCV, DECODE, false, 3><<<nb, 256, 0, st>>>(                       \
+                in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
+                out_gstride, tu);                                                             \
+        else if (s >= 4 && pd_choice() == 1)                                                  \
+            gf_apply_kernel<RCV, DECODE, false, 1><<<nb, 256, 0, st>>>(                       \
+                in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
+                out_gstride, tu);                                                             \
+        else if (s >= 4)                                                                      \
+            gf_apply_kernel<RCV, DECODE, false, 2><<<nb, 256, 0, st>>>(                       \
                 in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
                 out_gstride, tu);                                                             \
         else                                                                                  \
-            gf_apply_kernel<RCV, DECODE, true><<<nb, 256, 0, st>>>(                           \
+            gf_apply_kernel<RCV, DECODE, true, 1><<<nb, 256, 0, st>>>(                        \
                 in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
                 out_gstride, tu);                                                             \
     } while (0)
