@@ -19,8 +19,17 @@ HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(ROOT)include/quic_fec.h \
         $(ROOT)include/quic_fec_group.h $(ROOT)Makefile
 OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o
 
-.PHONY: all lib oracle clean
-all: lib oracle
+TOOL := $(ROOT)quic_amd/bin/fec_loopback
+
+.PHONY: all lib oracle tools clean
+all: lib oracle tools
+
+tools: $(TOOL)
+
+$(TOOL): $(ROOT)tools/loopback/fec_loopback.cpp $(LIB) $(ROOT)include/quic_fec_group.h
+	@mkdir -p $(ROOT)quic_amd/bin
+	g++ -O2 -std=c++17 -Wall -I$(ROOT)include -o $@ $< -L$(ROOT)quic_amd -lquic_fec \
+	    -Wl,-rpath,'$$ORIGIN/..' -ldl -lpthread
 
 lib: $(LIB)
 
@@ -43,5 +52,5 @@ oracle:
 	$(MAKE) -s -C $(ROOT)oracle
 
 clean:
-	rm -rf $(ROOT)build $(LIB)
+	rm -rf $(ROOT)build $(LIB) $(TOOL)
 	$(MAKE) -s -C $(ROOT)oracle clean

@@ -51,6 +51,13 @@ typedef struct qfec_group qfec_group;
 typedef struct qfec_packets qfec_packets;
 
 QFEC_API qfec_group *qfec_group_new(unsigned long long fec_group_number, int fec_configuration);
+/* Same, with an explicit codec of the cauchy_256 ABI (NULL, NULL = the GPU drop-ins).  Used
+ * by the loopback tool to run the reference CPU codec beside the GPU path. */
+typedef int (*qfec_encode_fn)(int, int, const unsigned char **, void *, int);
+typedef int (*qfec_decode_fn)(int, int, Block *, int);
+QFEC_API qfec_group *qfec_group_new_with_codec(unsigned long long fec_group_number,
+                                               int fec_configuration, qfec_encode_fn enc,
+                                               qfec_decode_fn dec);
 QFEC_API void qfec_group_free(qfec_group *g);
 QFEC_API int qfec_group_update_sent(qfec_group *g, int encryption_level, unsigned long long pn,
                                     int packet_number_len, const unsigned char *payload, size_t len);

@@ -65,8 +65,10 @@ static int round8(size_t n) { return (int)((n + 7) & ~(size_t)7); }
 
 class QuicFecGroup {
    public:
-    QuicFecGroup(uint64_t fec_group_number, int conf)
-        : fec_configuration(conf), min_(fec_group_number), eff_level_(kNumEncryptionLevels) {
+    QuicFecGroup(uint64_t fec_group_number, int conf, qfec_encode_fn enc = nullptr,
+                 qfec_decode_fn dec = nullptr)
+        : fec_configuration(conf), min_(fec_group_number), eff_level_(kNumEncryptionLevels),
+          enc_(enc ? enc : cauchy_256_encode), dec_(dec ? dec : cauchy_256_decode) {
         k_ = k_from_conf(conf);
         m_ = m_from_conf(conf);
         max_ = fec_group_number - 1 + k_;   // :93-94
@@ -159,12 +161,12 @@ class QuicFecGroup {
             if (status) *status = -2;
             return {};
         }
-        _cauchy_256_init(CAUCHY_256_VERSION);   // :342
+        if (enc_ == cauchy_256_encode) _cauchy_256_init(CAUCHY_256_VERSION);   // :342
         std::vector<const unsigned char*> ptrs(k_);
         for (size_t i = 0; i < k_; ++i) ptrs[i] = blocks.data() + i * bb;
         std::vector<unsigned char> rec((size_t)m_ * bb, 0);
         // always executed and checked (the reference wraps it in assert(), :378)
-        const int rc = cauchy_256_encode((int)k_, (int)m_, ptrs.data(), rec.data(), bb);
+        const int rc = enc_((int)k_, (int)m_, ptrs.data(), rec.data(), bb);
         SetRedundancy(rec.data(), bb, rc);
         have_red_ = false;
         if (status) *status = rc;
@@ -236,7 +238,7 @@ class QuicFecGroup {
             blk[i].data = blocks.data() + i * bb;
             blk[i].row = rows[i];
         }
-        const int rc = cauchy_256_decode((int)k_, (int)m_, blk.data(), bb);   // :277
+        const int rc = dec_((int)k_, (int)m_, blk.data(), bb);   // :277
         for (size_t i = 0; i < k_; ++i) rows[i] = blk[i].row;
         SetRevived(missing, blocks.data(), rows.data(), bb, rc);
         have_rev_ = false;
@@ -256,13 +258,16 @@ class QuicFecGroup {
     bool have_red_ = false, have_rev_ = false;
     int red_status_ = 0, rev_status_ = 0;
     std::vector<ParityPacket> red_, rev_;
+    qfec_encode_fn enc_;
+    qfec_decode_fn dec_;
 };
 
 }  // namespace qfec
 
 struct qfec_group {
     qfec::QuicFecGroup g;
-    qfec_group(unsigned long long n, int conf) : g(n, conf) {}
+    qfec_group(unsigned long long n, int conf, qfec_encode_fn e = nullptr, qfec_decode_fn d = nullptr)
+        : g(n, conf, e, d) {}
 };
 struct qfec_packets {
     std::vector<qfec::ParityPacket> v;
@@ -349,6 +354,10 @@ long qfec_prefix_payload(const unsigned char* p, size_t len, int pnlen, unsigned
 int qfec_block_bytes(size_t n) { return qfec::round8(n); }
 
 qfec_group* qfec_group_new(unsigned long long n, int conf) { return new qfec_group(n, conf); }
+qfec_group* qfec_group_new_with_codec(unsigned long long n, int conf, qfec_encode_fn e,
+                                      qfec_decode_fn d) {
+    return new qfec_group(n, conf, e, d);
+}
 void qfec_group_free(qfec_group* g) { delete g; }
 
 int qfec_group_update_sent(qfec_group* g, int level, unsigned long long pn, int pnlen,

@@ -23,6 +23,8 @@ _SIG = {
     "qfec_block_bytes": (_c.c_int, [_c.c_size_t]),
     "qfec_group_new": (_c.c_void_p, [_c.c_ulonglong, _c.c_int]),
     "qfec_group_free": (None, [_c.c_void_p]),
+    "qfec_group_new_with_codec": (_c.c_void_p, [_c.c_ulonglong, _c.c_int, _c.c_void_p,
+                                                _c.c_void_p]),
     "qfec_group_update_sent": (_c.c_int, [_c.c_void_p, _c.c_int, _c.c_ulonglong, _c.c_int,
                                           _c.c_char_p, _c.c_size_t]),
     "qfec_group_update_received": (_c.c_int, [_c.c_void_p, _c.c_int, _c.c_ulonglong, _c.c_int,
