@@ -63,6 +63,14 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built: run `make lib` (HIP extension required; "
                           "there is no CPU fallback)")
+    # One HIP runtime per process.  torch ships its own libamdhip64 (soname
+    # libamdhip64.so.7, the one libquic_fec.so asks for): loading torch first makes the
+    # dynamic linker bind our library to that copy.  Loaded the other way round, torch
+    # would bring up a second runtime and see no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(L, name)   # AttributeError if the export is missing

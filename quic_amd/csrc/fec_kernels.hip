@@ -979,11 +979,14 @@ static int pd_choice() {
     return pd;
 }
 
+// The LDS-staged GF kernel is opt-in (QFEC_STAGE=1): on MI355X it measured 2x slower
+// than the register-pipelined gf_apply_kernel on both (32, 4, 1352) and (128, 16, 9008)
+// (profiles/r01/README.md).
 static bool stage_disabled() {
     static int d = -1;
     if (d < 0) {
-        const char* e = getenv("QFEC_NO_STAGE");
-        d = e && atoi(e) ? 1 : 0;
+        const char* e = getenv("QFEC_STAGE");
+        d = e && atoi(e) ? 0 : 1;
     }
     return d;
 }
