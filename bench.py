@@ -110,7 +110,7 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from quic_amd import fec, synth
+    from quic_amd import fec, shard, synth
     k, m, payload, r, label = WORKLOADS[args.workload]
     bb = block_bytes(payload)
     G = args.groups
@@ -122,11 +122,12 @@ def main():
 
     # ---- resident inputs: this rank's shard [rank*G, (rank+1)*G) of the global workload
     data = torch.empty((G, k, bb), dtype=torch.uint8, device=dev)
-    fec.synth_fill(data, seed=seed, byte_offset=rank * G * k * bb)
+    g0, _ = shard.weak_range(G, rank)
+    fec.synth_fill(data, seed=seed, byte_offset=shard.data_byte_offset(g0, k, bb))
     parity = torch.zeros((G, m, bb), dtype=torch.uint8, device=dev)
     rc = eng.encode(k, m, bb, data, parity)
     assert rc == 0, rc
-    rows_np, src_np = synth.loss_patterns(k, m, r, G, seed + rank, mode="random",
+    rows_np, src_np = synth.loss_patterns(k, m, r, G, shard.loss_seed(seed, rank), mode="random",
                                           parity="random", shuffle=False)
     rows = torch.from_numpy(rows_np).to(dev)
     src = torch.from_numpy(src_np).to(dev)
@@ -166,14 +167,11 @@ def main():
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
 
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(elapsed, dev)
 
     ms_per_step = elapsed * 1e3 / args.steps
     total_groups = G * world
-    goodput = total_groups * k * payload / 2**30 / (elapsed / args.steps)
+    goodput = shard.aggregate_goodput_gib(G, world, k, payload, elapsed / args.steps)
 
     # algorithmic HBM bytes per launch: encode reads k, writes m blocks;
     # decode reads the k received blocks and writes the r recovered ones
