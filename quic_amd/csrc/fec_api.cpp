@@ -225,6 +225,11 @@ int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     const uint8_t* tab = nullptr;
     int rcode = get_enc_table(c, k, m, rc, &tab);
     if (rcode) return rcode;
+    if (qfec::gf_ring_supported(k, m, bb, rc, (m + rc - 1) / rc)) {
+        QF_HIP(qfec::launch_gf_ring(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc,
+                                    (m + rc - 1) / rc, 0, 0, (long long)m * bb, false, st));
+        return 0;
+    }
     QF_HIP(qfec::launch_gf_encode(d_data, d_par, tab, k, m, bb, G, rc, st));
     return 0;
 }
@@ -254,6 +259,15 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc, rmax,
                                     G, st));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
+    if (qfec::gf_ring_supported(k, m, bb, rc, nchunk)) {
+        // streams each group once and stores its recovered blocks after the group's last
+        // block is in LDS, so in place needs no scratch
+        const int rcp = std::max(rc, 4);
+        QF_HIP(qfec::launch_gf_ring(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
+                                    nchunk, rmax, (long long)nchunk * k * rcp,
+                                    (long long)k * bb, true, st));
+        return 0;
+    }
     if (nchunk > 1 && d_out == d_blocks && !qfec::gf_staged(d_blocks, k, bb, nchunk, rc)) {
         // in place with several output chunks: a later chunk would read slots an earlier
         // chunk already overwrote, so stage the recovered blocks first

@@ -24,6 +24,7 @@
 // W/Z recurrences used below.
 #include "fec_kernels.h"
 #include "gf256.h"
+#include "gf_bitslice.h"
 
 namespace qfec {
 
@@ -31,14 +32,6 @@ typedef uint32_t u32ua __attribute__((aligned(1)));   // unaligned dword (gfx950
 typedef uint64_t u64a __attribute__((aligned(8)));
 
 __constant__ GfTables c_gf = make_gf_tables();
-
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // v_bitop3_b32 ... bitop3:0x96
-}
-
-__device__ __forceinline__ int wave_id() {
-    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-}
 
 // ------------------------------------------------------------------ m = 1 XOR paths
 // Flat mapping: every lane owns one VS-byte unit (g, q) of one group and issues all k of
@@ -116,13 +109,6 @@ __global__ __launch_bounds__(256) void xor_flat_kernel(
     }
 }
 
-// LDS-DMA variant (the shipped m = 1 path when a group is 16-byte aligned and fits):
-// each wave owns groups g = w, w + W, ... and streams a whole group (k*bb contiguous
-// bytes) into one of two LDS slots with global_load_lds_dwordx4 nt (1 KiB per wave
-// instruction), XORs the k blocks from LDS while the next group's DMA is in flight, and
-// writes 8-byte nt stores.  Measured 6.15 TB/s cold on the (10, 1, 1352) layout vs
-// 4.5 TB/s for plain loads (tools/microbench/dma_variants.hip).  The whole group is in
-// LDS before any byte is written, so an in-place decode has no read/write hazard.
 #define QF_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define QF_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
@@ -130,99 +116,6 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits on gfx9");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-constexpr int kDmaWaves = 4;     // waves per workgroup (one per SIMD)
-constexpr int kDmaMaxKiB = 20;   // 4 waves x 2 slots x 20 KiB = 160 KiB of LDS
-
-// m = 1 decode bookkeeping for one group, done by the wave that decodes it (k <= 64,
-// one row tag per lane; cauchy_decode_m1, cauchy_256.cpp:486-540).  `r` is this lane's
-// row tag (lanes >= k hold 255).  Returns the erased slot (-1 if none) and writes
-// rows_out / status.
-__device__ __forceinline__ int m1_rows_wave(int r, int k, uint8_t* flags, uint8_t* ro,
-                                            int32_t* status, long long g) {
-    const int lane = threadIdx.x & 63;
-    const unsigned long long er = __ballot(lane < k && r >= k);
-    const int e = er ? __ffsll((long long)er) - 1 : -1;
-    flags[lane] = 0;
-    __builtin_amdgcn_wave_barrier();
-    if (lane < k && lane != e && r < k) flags[r] = 1;
-    __builtin_amdgcn_wave_barrier();
-    const unsigned long long miss = __ballot(lane < k && !flags[lane]);
-    if (lane < k) {
-        int v = r;
-        if (lane == e && miss) v = __ffsll((long long)miss) - 1;
-        ro[lane] = (uint8_t)v;
-    }
-    if (status && lane == 0) status[g] = 0;
-    return e;
-}
-
-template <int NDMA, bool DECODE>
-__global__ __launch_bounds__(kDmaWaves * 64) void xor_dma_kernel(
-    const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ eidx,
-    const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
-    int k, int bb, long long groups, long long out_gstride) {
-    constexpr int SLOT = NDMA * 1024;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int w = wave_id(), lane = threadIdx.x & 63;
-    uint8_t* myl = smem + (size_t)w * 2 * SLOT;
-    uint8_t* flags = smem + (size_t)kDmaWaves * 2 * SLOT + w * 64;
-    const long long W = (long long)gridDim.x * kDmaWaves;
-    long long g = (long long)blockIdx.x * kDmaWaves + w;
-    if (g >= groups) return;
-    const int gb = k * bb;
-    const bool fused = DECODE && rows_in != nullptr;   // rows handled here (k <= 64)
-    auto issue = [&](long long gg, int slot) {
-        const uint8_t* src = in + gg * gb;
-#pragma unroll
-        for (int i = 0; i < NDMA; ++i) {
-            const int off = min(i * 1024 + lane * 16, gb - 16);   // last piece: clamp inside
-            __builtin_amdgcn_global_load_lds(QF_GPTR(src + off),
-                                             QF_LPTR(myl + slot * SLOT + i * 1024), 16, 0, 2);
-        }
-    };
-    // The next group's row tags (or erased-slot index) are fetched before that group's
-    // DMA is issued, so the counted wait below also covers them.
-    auto fetch_rows = [&](long long gg) -> int {
-        if (!DECODE) return 0;
-        if (fused) return lane < k ? rows_in[gg * k + lane] : 255;
-        return eidx[gg];
-    };
-    int r_next = fetch_rows(g);
-    issue(g, 0);
-    int slot = 0;
-    const int nq = bb >> 3;
-    for (; g < groups; g += W) {
-        const long long gn = g + W;
-        const int r_cur = r_next;
-        if (gn < groups) {
-            r_next = fetch_rows(gn);
-            issue(gn, slot ^ 1);
-            wait_vmcnt<NDMA>();   // group g landed (the NDMA younger ops are group gn)
-        } else {
-            wait_vmcnt<0>();
-        }
-        int e = 0;
-        if (DECODE) {
-            e = fused ? m1_rows_wave(r_cur, k, flags, rows_out + g * k, status, g) : r_cur;
-            if (!fused && e == 255) e = -1;
-        }
-        if (!DECODE || e >= 0) {
-            const uint8_t* L = myl + slot * SLOT;
-            uint8_t* o = out + g * out_gstride + (long long)e * bb;
-            for (int q = lane; q < nq; q += 64) {
-                uint64_t acc = *(const uint64_t*)(L + q * 8);
-                int x = 1;
-                for (; x + 1 < k; x += 2)
-                    acc ^= *(const uint64_t*)(L + x * bb + q * 8) ^
-                           *(const uint64_t*)(L + (x + 1) * bb + q * 8);
-                if (x < k) acc ^= *(const uint64_t*)(L + x * bb + q * 8);
-                __builtin_nontemporal_store(acc, (uint64_t*)(o + q * 8));
-            }
-        }
-        slot ^= 1;
-    }
 }
 
 // Tiny blocks (bb < 4): one byte per lane.
@@ -304,54 +197,6 @@ __global__ void rows_k1_kernel(const uint8_t* __restrict__ rows_in, uint8_t* row
     rows_out[g] = 0;
     (void)rows_in;
     if (status) status[g] = 0;
-}
-
-// ------------------------------------------------------------- bit-sliced GF apply
-// For one input block, the lane holds its column word of the 8 sub-rows, W[0..7].
-// Extend to W[n] = <alpha^n, in> for n = 0..14 (linear in the input):
-//   alpha^(n) = alpha^(n-1) + alpha^(n-6) + alpha^(n-7) + alpha^(n-8)   (from 0x187)
-// and keep the pair sums Z[n] = W[n] ^ W[n+1].  A coefficient a = sum_b a_b alpha^b then
-// contributes  out[r] ^= XOR_{b : a_b} W[b + r]   (r = 0..7), i.e. per nibble p of a at
-// bit offset B a fixed XOR of at most two W/Z terms per output sub-row.
-struct WZ {
-    uint32_t W[15];
-    uint32_t Z[14];
-};
-
-__device__ __forceinline__ void expand_wz(WZ& v) {
-#pragma unroll
-    for (int i = 0; i < 7; ++i) v.Z[i] = v.W[i] ^ v.W[i + 1];
-#pragma unroll
-    for (int n = 8; n < 15; ++n) v.W[n] = xor3(v.W[n - 1], v.W[n - 6], v.Z[n - 8]);
-#pragma unroll
-    for (int i = 7; i < 14; ++i) v.Z[i] = v.W[i] ^ v.W[i + 1];
-}
-
-template <int B>
-__device__ __forceinline__ void apply_nibble(uint32_t (&acc)[8], uint32_t p, const WZ& v) {
-#define QF_CASE(P, EXPR)                                   \
-    case P:                                                \
-        _Pragma("unroll") for (int r = 0; r < 8; ++r) { acc[r] = EXPR; } \
-        break;
-    switch (p) {
-        QF_CASE(1, acc[r] ^ v.W[B + r])
-        QF_CASE(2, acc[r] ^ v.W[B + 1 + r])
-        QF_CASE(3, acc[r] ^ v.Z[B + r])
-        QF_CASE(4, acc[r] ^ v.W[B + 2 + r])
-        QF_CASE(5, xor3(acc[r], v.W[B + r], v.W[B + 2 + r]))
-        QF_CASE(6, acc[r] ^ v.Z[B + 1 + r])
-        QF_CASE(7, xor3(acc[r], v.Z[B + r], v.W[B + 2 + r]))
-        QF_CASE(8, acc[r] ^ v.W[B + 3 + r])
-        QF_CASE(9, xor3(acc[r], v.W[B + r], v.W[B + 3 + r]))
-        QF_CASE(10, xor3(acc[r], v.W[B + 1 + r], v.W[B + 3 + r]))
-        QF_CASE(11, xor3(acc[r], v.Z[B + r], v.W[B + 3 + r]))
-        QF_CASE(12, acc[r] ^ v.Z[B + 2 + r])
-        QF_CASE(13, xor3(acc[r], v.W[B + r], v.Z[B + 2 + r]))
-        QF_CASE(14, xor3(acc[r], v.Z[B + 1 + r], v.W[B + 3 + r]))
-        QF_CASE(15, xor3(acc[r], v.Z[B + r], v.Z[B + 2 + r]))
-        default: break;
-    }
-#undef QF_CASE
 }
 
 // Column-word access.  Word c of sub-row t covers bytes [t*s + 4c, +4); the last word of a
@@ -871,51 +716,12 @@ static int num_cus() {
     return n;
 }
 
-struct RowsIO {
-    const uint8_t* rows_in;   // non-null: decode kernel does the m = 1 bookkeeping itself
-    uint8_t* rows_out;
-    int32_t* status;
-};
-
-template <bool DECODE, int N>
-static void xor_dma_launch_n(int ndma, const uint8_t* in, uint8_t* out, const uint8_t* eidx,
-                             RowsIO rio, int k, int bb, long long G, long long ogs,
-                             hipStream_t st) {
-    if constexpr (N > kDmaMaxKiB) {
-        return;
-    } else {
-        if (ndma != N)
-            return xor_dma_launch_n<DECODE, N + 1>(ndma, in, out, eidx, rio, k, bb, G, ogs, st);
-        const size_t lds = (size_t)kDmaWaves * 2 * N * 1024 + kDmaWaves * 64;
-        const long long want = (G + kDmaWaves - 1) / kDmaWaves;
-        const unsigned nb = (unsigned)std::min<long long>(want, (long long)num_cus());
-        xor_dma_kernel<N, DECODE><<<nb, kDmaWaves * 64, lds, st>>>(
-            in, out, eidx, rio.rows_in, rio.rows_out, rio.status, k, bb, G, ogs);
-    }
-}
-
-static bool xor_dma_ok(const void* in, const void* out, int k, int bb, long long ogs) {
-    static int disabled = -1;
-    if (disabled < 0) {
-        const char* e = getenv("QFEC_NO_DMA");
-        disabled = e && atoi(e) ? 1 : 0;
-    }
-    const long long gb = (long long)k * bb;
-    return !disabled && bb % 8 == 0 && gb % 16 == 0 && gb >= 16 &&
-           ((uintptr_t)in & 15) == 0 && (((uintptr_t)out | (uintptr_t)ogs) & 7) == 0 &&
-           (gb + 1023) / 1024 + 1 <= kDmaMaxKiB;
-}
-
 template <bool DECODE>
 static hipError_t xor_any(const uint8_t* in, uint8_t* out, const uint8_t* eidx, int k, int bb,
                           long long G, long long igs, long long ogs, hipStream_t st) {
     if (G <= 0) return hipSuccess;
-    if (igs == (long long)k * bb && xor_dma_ok(in, out, k, bb, ogs)) {
-        const int ndma = (int)((igs + 1023) / 1024);
-        xor_dma_launch_n<DECODE, 1>(ndma, in, out, eidx, RowsIO{nullptr, nullptr, nullptr}, k,
-                                    bb, G, ogs, st);
-        return hipGetLastError();
-    }
+    if (igs == (long long)k * bb && xor_dma_ok(in, out, k, bb, ogs))
+        return launch_xor_dma(in, out, eidx, nullptr, nullptr, nullptr, k, bb, G, ogs, DECODE, st);
     const int vs = xor_unit(in, out, igs, ogs, bb);
     const long long units = G * ((bb + vs - 1) / vs);
     if (units > 0xffffffffLL) return hipErrorInvalidValue;
@@ -936,13 +742,10 @@ hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t*
                              long long groups, hipStream_t st) {
     if (groups <= 0) return hipSuccess;
     const long long gb = (long long)k * bb;
-    if (k <= 64 && xor_dma_ok(blocks, out, k, bb, gb)) {
+    if (k <= 64 && xor_dma_ok(blocks, out, k, bb, gb))
         // single launch: the DMA kernel also does the erased-slot / missing-row bookkeeping
-        const int ndma = (int)((gb + 1023) / 1024);
-        xor_dma_launch_n<true, 1>(ndma, blocks, out, nullptr, RowsIO{rows_in, rows_out, status},
-                                  k, bb, groups, gb, st);
-        return hipGetLastError();
-    }
+        return launch_xor_dma(blocks, out, nullptr, rows_in, rows_out, status, k, bb, groups, gb,
+                              true, st);
     m1_prep_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(rows_in, rows_out, status,
                                                                      eidx, k, groups);
     hipError_t e = hipGetLastError();

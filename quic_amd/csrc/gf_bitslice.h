@@ -1,0 +1,68 @@
+// gf_bitslice.h — bit-sliced GF(2^8) helpers shared by the gfx950 FEC kernels.
+//
+// A block of bb bytes is 8 sub-rows of s = bb/8 bytes; byte column j of the 8 sub-rows
+// is one bit-sliced vector (cauchy_256.cpp:90-125).  A lane holds one 4-byte column word
+// of each sub-row, W[0..7]; everything below is v_xor / v_bitop3 on those words.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qfec {
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // v_bitop3_b32 ... bitop3:0x96
+}
+
+__device__ __forceinline__ int wave_id() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+// ------------------------------------------------------------- bit-sliced GF apply
+// For one input block, the lane holds its column word of the 8 sub-rows, W[0..7].
+// Extend to W[n] = <alpha^n, in> for n = 0..14 (linear in the input):
+//   alpha^(n) = alpha^(n-1) + alpha^(n-6) + alpha^(n-7) + alpha^(n-8)   (from 0x187)
+// and keep the pair sums Z[n] = W[n] ^ W[n+1].  A coefficient a = sum_b a_b alpha^b then
+// contributes  out[r] ^= XOR_{b : a_b} W[b + r]   (r = 0..7), i.e. per nibble p of a at
+// bit offset B a fixed XOR of at most two W/Z terms per output sub-row.
+struct WZ {
+    uint32_t W[15];
+    uint32_t Z[14];
+};
+
+__device__ __forceinline__ void expand_wz(WZ& v) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) v.Z[i] = v.W[i] ^ v.W[i + 1];
+#pragma unroll
+    for (int n = 8; n < 15; ++n) v.W[n] = xor3(v.W[n - 1], v.W[n - 6], v.Z[n - 8]);
+#pragma unroll
+    for (int i = 7; i < 14; ++i) v.Z[i] = v.W[i] ^ v.W[i + 1];
+}
+
+template <int B>
+__device__ __forceinline__ void apply_nibble(uint32_t (&acc)[8], uint32_t p, const WZ& v) {
+#define QF_CASE(P, EXPR)                                   \
+    case P:                                                \
+        _Pragma("unroll") for (int r = 0; r < 8; ++r) { acc[r] = EXPR; } \
+        break;
+    switch (p) {
+        QF_CASE(1, acc[r] ^ v.W[B + r])
+        QF_CASE(2, acc[r] ^ v.W[B + 1 + r])
+        QF_CASE(3, acc[r] ^ v.Z[B + r])
+        QF_CASE(4, acc[r] ^ v.W[B + 2 + r])
+        QF_CASE(5, xor3(acc[r], v.W[B + r], v.W[B + 2 + r]))
+        QF_CASE(6, acc[r] ^ v.Z[B + 1 + r])
+        QF_CASE(7, xor3(acc[r], v.Z[B + r], v.W[B + 2 + r]))
+        QF_CASE(8, acc[r] ^ v.W[B + 3 + r])
+        QF_CASE(9, xor3(acc[r], v.W[B + r], v.W[B + 3 + r]))
+        QF_CASE(10, xor3(acc[r], v.W[B + 1 + r], v.W[B + 3 + r]))
+        QF_CASE(11, xor3(acc[r], v.Z[B + r], v.W[B + 3 + r]))
+        QF_CASE(12, acc[r] ^ v.Z[B + 2 + r])
+        QF_CASE(13, xor3(acc[r], v.W[B + r], v.Z[B + 2 + r]))
+        QF_CASE(14, xor3(acc[r], v.Z[B + 1 + r], v.W[B + 3 + r]))
+        QF_CASE(15, xor3(acc[r], v.Z[B + r], v.Z[B + 2 + r]))
+        default: break;
+    }
+#undef QF_CASE
+}
+
+}  // namespace qfec
