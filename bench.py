@@ -83,6 +83,89 @@ def cpu_baseline(k, m, bb, payload, r, data_h, blocks_h, rows_h, seconds):
     }
 
 
+# Which template argument of each kernel says "decode" (bool): the PMC summaries are split
+# into the encode and the decode phase by it.
+_DECODE_ARG = {"xor_dma_kernel": 2, "gf_apply_kernel": 1, "gf_ring_kernel": 5,
+               "gf_stage_kernel": 1}
+_DECODE_ONLY = ("decode_prep_kernel", "m1_prep_kernel", "scatter_recovered_kernel",
+                "rows_k1_kernel")
+
+
+def _phase(name):
+    base = name.split("(")[0].replace("void ", "").replace("qfec::", "").strip()
+    kern = base.split("<")[0]
+    if kern.startswith("synth_"):
+        return None
+    if kern in _DECODE_ONLY:
+        return "decode"
+    if kern in _DECODE_ARG and "<" in base:
+        args = [a.strip() for a in base[base.index("<") + 1:base.rindex(">")].split(",")]
+        return "decode" if args[_DECODE_ARG[kern]] == "true" else "encode"
+    return "encode" if kern == "replicate_kernel" else None
+
+
+def pmc_traffic(workload, phase, groups):
+    """HBM bytes per launch of `phase` from the newest committed PMC summary
+    (profiles/r*/pmc_<workload>.json, written by tools/pmc_summary.py), scaled to
+    `groups`.  None when no summary covers this workload."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{workload}.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    tot = 0
+    for name, e in d["kernels"].items():
+        if _phase(name) == phase and "traffic_bytes" in e:
+            tot += e["traffic_bytes"]
+    if not tot:
+        return None, None
+    return round(tot * groups / d["groups"]), os.path.relpath(files[-1], ROOT)
+
+
+def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps):
+    """Host-resident rate: pinned host buffers in and out, H2D + kernels + D2H through the
+    library's pipelined host-pointer entry points (qfec_*_batch_host).  Never `value`."""
+    import torch
+    from quic_amd import fec
+    G = data.shape[0]
+    data_h = torch.empty(data.shape, dtype=torch.uint8, pin_memory=True)
+    data_h.copy_(data)
+    parity_h = torch.empty((G, m, bb), dtype=torch.uint8, pin_memory=True)
+    blocks0 = torch.empty(blocks.shape, dtype=torch.uint8, pin_memory=True)
+    blocks0.copy_(blocks)
+    rows0 = rows.cpu()
+    blocks_h = torch.empty_like(blocks0).pin_memory()
+    rows_h = torch.empty_like(rows0).pin_memory()
+    status_h = torch.zeros((G,), dtype=torch.int32).pin_memory()
+    t_enc = t_dec = 0.0
+    for i in range(steps + 1):
+        blocks_h.copy_(blocks0)
+        rows_h.copy_(rows0)
+        t0 = time.perf_counter()
+        fec.encode_host_into(eng, k, m, bb, data_h, parity_h)
+        t1 = time.perf_counter()
+        fec.decode_host_into(eng, k, m, bb, blocks_h, rows_h, status_h)
+        t2 = time.perf_counter()
+        if i:                      # first pass warms the staging buffers
+            t_enc += t1 - t0
+            t_dec += t2 - t1
+    ok = int(status_h.abs().max()) == 0
+    pcie = G * (k * bb + m * bb) + G * (2 * k * bb + 2 * k + 4)
+    return {
+        "value": round(G * k * payload / 2**30 / ((t_enc + t_dec) / steps), 3),
+        "unit": "GiB/s",
+        "encode_ms": round(t_enc / steps * 1e3, 3),
+        "decode_ms": round(t_dec / steps * 1e3, 3),
+        "pcie_bytes_per_step": pcie,
+        "pcie_GBps": round(pcie / ((t_enc + t_dec) / steps) / 1e9, 2),
+        "status_ok": ok,
+        "note": "pinned host buffers; qfec_encode_batch_host + qfec_decode_batch_host "
+                "(in place, cauchy_256_decode semantics), 64 MiB chunks, H2D/kernel/D2H "
+                "pipelined; not the bench value",
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,6 +177,8 @@ def main():
     ap.add_argument("--cpu-groups", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check recovered data after timing")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) leg")
+    ap.add_argument("--host-steps", type=int, default=3)
     args = ap.parse_args()
 
     import torch
@@ -181,6 +266,11 @@ def main():
     dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
     step_gbs = (enc_bytes + dec_bytes) / (enc_ms + dec_ms) / 1e6
     if enc_ms >= dec_ms:
+        phase = "encode"
+    else:
+        phase = "decode"
+    traffic, traffic_src = pmc_traffic(args.workload, phase, G)
+    if enc_ms >= dec_ms:
         dom = ("encode", "xor_encode_kernel" if m == 1 else "gf_apply_kernel<encode>",
                enc_gbs, enc_bytes)
     else:
@@ -199,6 +289,10 @@ def main():
         n = min(args.cpu_groups, G)
         cpu = cpu_baseline(k, m, bb, payload, r, data[:n].cpu().numpy(),
                            blocks[:n].cpu().numpy(), rows_np[:n], args.cpu_seconds)
+
+    host = None
+    if rank == 0 and world == 1 and not args.no_host:
+        host = host_inclusive(eng, k, m, bb, payload, data, blocks, rows, args.host_steps)
 
     if rank == 0:
         line = {
@@ -230,7 +324,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(dom[2] / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": dom[3],
             },
             "kernels": {
@@ -240,6 +335,7 @@ def main():
                 "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4),
             },
             "cpu_baseline": cpu,
+            "host_inclusive": host,
         }
         if verified is not None:
             line["verified"] = verified

@@ -137,6 +137,12 @@ struct qfec_ctx {
     DevBuf dcoef, dslots, dnout, dscratch;
     HostBuf h_stage;
     DevBuf d_stage;
+    // host-pointer batches: copy-in / copy-out streams around `stream` (compute), NB
+    // rotating device staging buffers so H2D, kernels and D2H of successive chunks overlap
+    static constexpr int NB = 3;
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    hipEvent_t ev_in[NB] = {}, ev_done[NB] = {}, ev_out[NB] = {};
+    DevBuf pbuf[NB];
     std::mutex mu;   // one caller at a time per context (the reference is single-threaded)
 };
 
@@ -282,6 +288,51 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     return 0;
 }
 
+// Host-pointer batches, chunked and pipelined: chunk i's H2D (s_in), kernels (stream)
+// and D2H (s_out) are ordered by events, and NB staging buffers rotate, so the copy-in of
+// chunk i + 1 and the copy-out of chunk i - 1 overlap the kernels of chunk i (PCIe is
+// full duplex).  The kernels of all chunks stay on one stream, so the decode workspace is
+// never shared by two chunks in flight.  Chunk size: QFEC_HOST_CHUNK_MB (default 64).
+// fn(g0, n, buf, phase): phase 0 enqueues the H2D, 1 the kernels, 2 the D2H.
+template <class F>
+int host_pipeline(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
+    if (!c->s_in) {
+        QF_HIP(hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking));
+        QF_HIP(hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
+        for (int b = 0; b < qfec_ctx::NB; ++b) {
+            QF_HIP(hipEventCreateWithFlags(&c->ev_in[b], hipEventDisableTiming));
+            QF_HIP(hipEventCreateWithFlags(&c->ev_done[b], hipEventDisableTiming));
+            QF_HIP(hipEventCreateWithFlags(&c->ev_out[b], hipEventDisableTiming));
+        }
+    }
+    const char* e = getenv("QFEC_HOST_CHUNK_MB");
+    const size_t target = (size_t)(e && atoi(e) > 0 ? atoi(e) : 64) << 20;
+    const long long chunk = std::max<long long>(1, std::min<long long>(groups, (long long)(target / per_group)));
+    const size_t bytes = (size_t)chunk * per_group + 16;
+    for (int b = 0; b < qfec_ctx::NB; ++b) QF_HIP(c->pbuf[b].ensure(bytes));
+    int i = 0;
+    for (long long g0 = 0; g0 < groups; g0 += chunk, ++i) {
+        const long long n = std::min(chunk, groups - g0);
+        const int b = i % qfec_ctx::NB;
+        uint8_t* buf = (uint8_t*)c->pbuf[b].p;
+        if (i >= qfec_ctx::NB) QF_HIP(hipStreamWaitEvent(c->s_in, c->ev_out[b], 0));
+        int r = fn(g0, n, buf, 0);
+        if (r) return r;
+        QF_HIP(hipEventRecord(c->ev_in[b], c->s_in));
+        QF_HIP(hipStreamWaitEvent(c->stream, c->ev_in[b], 0));
+        if ((r = fn(g0, n, buf, 1))) {
+            (void)hipStreamSynchronize(c->s_out);
+            return r;
+        }
+        QF_HIP(hipEventRecord(c->ev_done[b], c->stream));
+        QF_HIP(hipStreamWaitEvent(c->s_out, c->ev_done[b], 0));
+        if ((r = fn(g0, n, buf, 2))) return r;
+        QF_HIP(hipEventRecord(c->ev_out[b], c->s_out));
+    }
+    QF_HIP(hipStreamSynchronize(c->s_out));
+    return 0;
+}
+
 // Default context for the single-group drop-ins (created on the caller's current device).
 std::once_flag g_default_once;
 qfec_ctx* g_default = nullptr;
@@ -330,8 +381,13 @@ int qfec_ctx_create(int device, qfec_ctx** out) {
 void qfec_ctx_destroy(qfec_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    for (hipStream_t s : {c->stream, c->s_in, c->s_out})
+        if (s) (void)hipStreamSynchronize(s);
+    for (int b = 0; b < qfec_ctx::NB; ++b)
+        for (hipEvent_t e : {c->ev_in[b], c->ev_done[b], c->ev_out[b]})
+            if (e) (void)hipEventDestroy(e);
+    for (hipStream_t s : {c->stream, c->s_in, c->s_out})
+        if (s) (void)hipStreamDestroy(s);
     delete c;
 }
 
@@ -367,27 +423,32 @@ int qfec_encode_batch_host(qfec_ctx* c, int k, int m, int bb, long long groups,
     if (!h_data || !h_parity) return fail(-2, "null buffer");
     std::lock_guard<std::mutex> lk(c->mu);
     if ((rc = set_device(c))) return rc;
-    // chunk the batch so the device staging stays bounded (~1 GiB)
-    const size_t per = (size_t)(k + m) * bb;
-    const long long step = std::max<long long>(1, (long long)((1ull << 30) / per));
-    const long long chunk = std::min(groups, step);
-    QF_HIP(c->d_stage.ensure((size_t)chunk * per));
-    uint8_t* dd = (uint8_t*)c->d_stage.p;
-    uint8_t* dp = dd + (size_t)chunk * k * bb;
+    // On the reference's -1 path only P0 is written (cauchy_256.cpp:1519-1534): copy back
+    // only row 0 of each group so the caller's other recovery rows stay untouched.
+    const bool p0_only = m > 1 && k > 1 && (k + m > 256 || bb % 8 != 0);
+    const size_t in_g = (size_t)k * bb, out_g = (size_t)m * bb;
     int result = 0;
-    for (long long g0 = 0; g0 < groups; g0 += chunk) {
-        const long long n = std::min(chunk, groups - g0);
-        QF_HIP(hipMemcpyAsync(dd, h_data + (size_t)g0 * k * bb, (size_t)n * k * bb,
-                              hipMemcpyHostToDevice, c->stream));
-        if (m > 1 && k > 1) QF_HIP(hipMemsetAsync(dp, 0, (size_t)n * m * bb, c->stream));
-        const int r = encode_impl(c, k, m, bb, n, dd, dp, c->stream);
-        if (r < -1) return r;
-        if (r) result = r;
-        QF_HIP(hipMemcpyAsync(h_parity + (size_t)g0 * m * bb, dp, (size_t)n * m * bb,
-                              hipMemcpyDeviceToHost, c->stream));
-    }
-    QF_HIP(hipStreamSynchronize(c->stream));
-    return result;
+    rc = host_pipeline(c, groups, in_g + out_g, [&](long long g0, long long n, uint8_t* buf,
+                                                     int phase) -> int {
+        uint8_t* dd = buf;
+        uint8_t* dp = buf + (size_t)n * in_g;
+        if (phase == 0) {
+            QF_HIP(hipMemcpyAsync(dd, h_data + (size_t)g0 * in_g, (size_t)n * in_g,
+                                  hipMemcpyHostToDevice, c->s_in));
+        } else if (phase == 1) {
+            const int r = encode_impl(c, k, m, bb, n, dd, dp, c->stream);
+            if (r < -1) return r;
+            if (r) result = r;
+        } else if (p0_only) {
+            QF_HIP(hipMemcpy2DAsync(h_parity + (size_t)g0 * out_g, out_g, dp, out_g, bb, n,
+                                    hipMemcpyDeviceToHost, c->s_out));
+        } else {
+            QF_HIP(hipMemcpyAsync(h_parity + (size_t)g0 * out_g, dp, (size_t)n * out_g,
+                                  hipMemcpyDeviceToHost, c->s_out));
+        }
+        return 0;
+    });
+    return rc ? rc : result;
 }
 
 int qfec_decode_batch_host(qfec_ctx* c, int k, int m, int bb, long long groups,
@@ -398,33 +459,33 @@ int qfec_decode_batch_host(qfec_ctx* c, int k, int m, int bb, long long groups,
     if (!h_blocks || !h_rows) return fail(-2, "null buffer");
     std::lock_guard<std::mutex> lk(c->mu);
     if ((rc = set_device(c))) return rc;
-    const size_t per = (size_t)k * bb + k + sizeof(int32_t);
-    const long long step = std::max<long long>(1, (long long)((1ull << 30) / per));
-    const long long chunk = std::min(groups, step);
-    QF_HIP(c->d_stage.ensure((size_t)chunk * per + 16));
-    uint8_t* db = (uint8_t*)c->d_stage.p;
-    uint8_t* dr = db + (size_t)chunk * k * bb;
-    int32_t* ds = (int32_t*)(((uintptr_t)(dr + (size_t)chunk * k) + 3) & ~(uintptr_t)3);
-    std::vector<int32_t> st_tmp;
-    for (long long g0 = 0; g0 < groups; g0 += chunk) {
-        const long long n = std::min(chunk, groups - g0);
-        QF_HIP(hipMemcpyAsync(db, h_blocks + (size_t)g0 * k * bb, (size_t)n * k * bb,
-                              hipMemcpyHostToDevice, c->stream));
-        QF_HIP(hipMemcpyAsync(dr, h_rows + (size_t)g0 * k, (size_t)n * k, hipMemcpyHostToDevice,
-                              c->stream));
-        const int r = decode_impl(c, k, m, bb, n, db, dr, db, dr, ds, c->stream);
-        if (r) return r;
-        QF_HIP(hipMemcpyAsync(h_blocks + (size_t)g0 * k * bb, db, (size_t)n * k * bb,
-                              hipMemcpyDeviceToHost, c->stream));
-        QF_HIP(hipMemcpyAsync(h_rows + (size_t)g0 * k, dr, (size_t)n * k, hipMemcpyDeviceToHost,
-                              c->stream));
-        if (h_status) {
-            QF_HIP(hipMemcpyAsync(h_status + g0, ds, (size_t)n * sizeof(int32_t),
-                                  hipMemcpyDeviceToHost, c->stream));
+    const size_t blk_g = (size_t)k * bb;
+    // per group: blocks, row tags, status (4-byte aligned inside the chunk buffer)
+    const size_t per = blk_g + k + sizeof(int32_t);
+    return host_pipeline(c, groups, per, [&](long long g0, long long n, uint8_t* buf,
+                                             int phase) -> int {
+        uint8_t* db = buf;
+        uint8_t* dr = db + (size_t)n * blk_g;
+        int32_t* ds = (int32_t*)(((uintptr_t)(dr + (size_t)n * k) + 3) & ~(uintptr_t)3);
+        if (phase == 0) {
+            QF_HIP(hipMemcpyAsync(db, h_blocks + (size_t)g0 * blk_g, (size_t)n * blk_g,
+                                  hipMemcpyHostToDevice, c->s_in));
+            QF_HIP(hipMemcpyAsync(dr, h_rows + (size_t)g0 * k, (size_t)n * k,
+                                  hipMemcpyHostToDevice, c->s_in));
+        } else if (phase == 1) {
+            const int r = decode_impl(c, k, m, bb, n, db, dr, db, dr, ds, c->stream);
+            if (r) return r;
+        } else {
+            QF_HIP(hipMemcpyAsync(h_blocks + (size_t)g0 * blk_g, db, (size_t)n * blk_g,
+                                  hipMemcpyDeviceToHost, c->s_out));
+            QF_HIP(hipMemcpyAsync(h_rows + (size_t)g0 * k, dr, (size_t)n * k,
+                                  hipMemcpyDeviceToHost, c->s_out));
+            if (h_status)
+                QF_HIP(hipMemcpyAsync(h_status + g0, ds, (size_t)n * sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, c->s_out));
         }
-    }
-    QF_HIP(hipStreamSynchronize(c->stream));
-    return 0;
+        return 0;
+    });
 }
 
 int qfec_synth_fill(void* d_dst, unsigned long long bytes, unsigned long long seed,

@@ -243,12 +243,16 @@ __device__ __forceinline__ void store_word(uint8_t* sub, int c, const ColAccess&
     }
 }
 
+// Workgroup-size bound per output-chunk width: it caps VGPRs at 512 / ceil(waves / 4), so
+// the RC x 8 accumulators never spill (RC 4: 128 VGPR, RC 8: 170, RC 16: 256).
+template <int RC> struct StageBound { static constexpr int T = RC <= 4 ? 1024 : (RC == 8 ? 640 : 320); };
+
 // One wave = one (group, output chunk, 64-word column tile).  RC outputs per wave.
 //   coef:  [(g) * coef_gstride + (chunk * k + pos) * RCP + j]  (RCP = max(4, RC))
 //   encode: outputs o = chunk*RC + j < m go to out + g*out_gstride + o*bb
 //   decode: outputs o < nout[g] go to out + g*out_gstride + slots[g*rmax + o]*bb
 template <int RC, bool DECODE, bool TINY, int PD>
-__global__ __launch_bounds__(256) void gf_apply_kernel(
+__global__ __launch_bounds__(StageBound<RC>::T) void gf_apply_kernel(
     const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, int k, int m, int bb,
     int nw, int ntiles, int nchunk, int rmax, long long coef_gstride, long long out_gstride,
@@ -256,7 +260,14 @@ __global__ __launch_bounds__(256) void gf_apply_kernel(
     constexpr int RCP = RC < 4 ? 4 : RC;
     constexpr int NCW = RCP / 4;
     const int lane = threadIdx.x & 63;
-    const int unit = blockIdx.x * 4 + wave_id();
+    // Units are numbered (group, chunk, tile) with the tile fastest; a workgroup holds 4
+    // consecutive units.  The chunks of a group re-read the same input blocks, so the
+    // workgroups of one group should share an L2: hardware deals workgroups round-robin
+    // to the 8 XCDs (each with its own L2), so logical workgroup l runs as hardware
+    // block b with consecutive l on one XCD (a bijection for any grid size).
+    const unsigned nbk = gridDim.x, b = blockIdx.x, xcd = b & 7u, q8 = nbk >> 3, r8 = nbk & 7u;
+    const unsigned lwg = xcd * q8 + (xcd < r8 ? xcd : r8) + (b >> 3);
+    const int unit = (int)lwg * 4 + wave_id();
     if (unit >= total_units) return;
     const int tile = unit % ntiles;
     const int gc = unit / ntiles;
@@ -354,9 +365,6 @@ __device__ __forceinline__ void wait_vmcnt_dyn(int n) {
 
 constexpr int kStageSlots = 4;   // ring depth: 3 blocks in flight while one is combined
 
-// Workgroup-size bound per output-chunk width: it caps VGPRs at 512 / ceil(waves / 4), so
-// the RC x 8 accumulators never spill (RC 4: 128 VGPR, RC 8: 170, RC 16: 256).
-template <int RC> struct StageBound { static constexpr int T = RC <= 4 ? 1024 : (RC == 8 ? 640 : 320); };
 
 template <int RC, bool DECODE>
 __global__ __launch_bounds__(StageBound<RC>::T) void gf_stage_kernel(
@@ -830,24 +838,27 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
 #undef QF_STAGE
         return hipGetLastError();
     }
+    const int per_group = nchunk * ntiles;
     const unsigned nb = blocks_for_waves(units);
+    const unsigned nthr = 256;
+    (void)per_group;
     const int tu = (int)units;
 #define QF_LAUNCH(RCV)                                                                        \
     do {                                                                                      \
         if (s >= 4 && pd_choice() == 3)                                                       \
-            gf_apply_kernel<RCV, DECODE, false, 3><<<nb, 256, 0, st>>>(                       \
+            gf_apply_kernel<RCV, DECODE, false, 3><<<nb, nthr, 0, st>>>(                      \
                 in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
                 out_gstride, tu);                                                             \
         else if (s >= 4 && pd_choice() == 1)                                                  \
-            gf_apply_kernel<RCV, DECODE, false, 1><<<nb, 256, 0, st>>>(                       \
+            gf_apply_kernel<RCV, DECODE, false, 1><<<nb, nthr, 0, st>>>(                      \
                 in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
                 out_gstride, tu);                                                             \
         else if (s >= 4)                                                                      \
-            gf_apply_kernel<RCV, DECODE, false, 2><<<nb, 256, 0, st>>>(                       \
+            gf_apply_kernel<RCV, DECODE, false, 2><<<nb, nthr, 0, st>>>(                      \
                 in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
                 out_gstride, tu);                                                             \
         else                                                                                  \
-            gf_apply_kernel<RCV, DECODE, true, 1><<<nb, 256, 0, st>>>(                        \
+            gf_apply_kernel<RCV, DECODE, true, 1><<<nb, nthr, 0, st>>>(                       \
                 in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
                 out_gstride, tu);                                                             \
     } while (0)

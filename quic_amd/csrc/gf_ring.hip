@@ -359,7 +359,7 @@ hipError_t ring_run(const RingPlan& p, int rc, bool dry, hipStream_t st) {
 
 RingPlan make_plan(int k, int m, int bb, int rc, int nchunk) {
     RingPlan p;
-    if (env_int("QFEC_NO_RING", 0)) return p;
+    if (!env_int("QFEC_RING", 0)) return p;   // opt-in: slower than gf_apply so far
     RingArgs& a = p.a;
     a.k = k; a.m = m; a.bb = bb; a.s = bb / 8;
     if (a.s < 4 || k < 1) return p;

@@ -174,6 +174,34 @@ class FecEngine:
         return blocks, rows, status
 
 
+def _hptr(t):
+    import torch
+    if not isinstance(t, torch.Tensor) or t.is_cuda or not t.is_contiguous():
+        raise TypeError("host buffers must be contiguous CPU tensors (pinned for full speed)")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def encode_host_into(engine, k, m, block_bytes, data_h, parity_h):
+    """Host-pointer encode on caller-owned CPU tensors (pinned memory recommended):
+    H2D, kernels and D2H pipelined in chunks inside the library.  Returns 0 / -1."""
+    rc = engine.lib.qfec_encode_batch_host(engine._h, k, m, block_bytes, data_h.shape[0],
+                                           _hptr(data_h), _hptr(parity_h))
+    if rc < -1:
+        raise FecError(rc, "qfec_encode_batch_host")
+    return rc
+
+
+def decode_host_into(engine, k, m, block_bytes, blocks_h, rows_h, status_h=None):
+    """Host-pointer in-place decode on caller-owned CPU tensors (cauchy_256_decode
+    semantics per group)."""
+    rc = engine.lib.qfec_decode_batch_host(engine._h, k, m, block_bytes, blocks_h.shape[0],
+                                           _hptr(blocks_h), _hptr(rows_h),
+                                           None if status_h is None else _hptr(status_h))
+    if rc:
+        raise FecError(rc, "qfec_decode_batch_host")
+    return rc
+
+
 def synth_fill(t, seed, byte_offset=0, stream=None):
     """Fill a device tensor with the seeded splitmix64 stream (quic_amd.synth)."""
     rc = load().qfec_synth_fill(_dptr(t), t.numel() * t.element_size(), seed, byte_offset,

@@ -1,0 +1,6 @@
+export TMPDIR=/tmp
+tools/gpu_session.sh \
+ "pytest_gpu::400::python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" \
+ "benchB::200::python bench.py --workload B --verify --no-cpu-baseline --no-host" \
+ "benchD::300::python bench.py --workload D --groups 16384 --steps 5 --warmup 2 --verify --no-cpu-baseline --no-host" \
+ "pmcD::400::bash tools/pmc.sh D r01g --groups 16384"
