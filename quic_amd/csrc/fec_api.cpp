@@ -97,7 +97,14 @@ int pow2_at_least(int v) {
     while (p < v) p <<= 1;
     return p;
 }
-int encode_rc(int m) { return std::min(pow2_at_least(m), 8); }
+int encode_rc(int m) {
+    static const int cap = [] {
+        const char* e = getenv("QFEC_ENC_RC");   // 2, 4 or 8 (tuning)
+        const int v = e ? atoi(e) : 8;
+        return (v == 2 || v == 4 || v == 8) ? v : 8;
+    }();
+    return std::min(pow2_at_least(m), cap);
+}
 int decode_rc(int rmax) { return std::min(pow2_at_least(rmax), 8); }
 
 struct DevBuf {
@@ -231,9 +238,9 @@ int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     const uint8_t* tab = nullptr;
     int rcode = get_enc_table(c, k, m, rc, &tab);
     if (rcode) return rcode;
-    if (qfec::gf_ring_supported(k, m, bb, rc, (m + rc - 1) / rc)) {
-        QF_HIP(qfec::launch_gf_ring(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc,
-                                    (m + rc - 1) / rc, 0, 0, (long long)m * bb, false, st));
+    if (qfec::gf_group_supported(k, m, bb, rc)) {
+        QF_HIP(qfec::launch_gf_group(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc,
+                                     (m + rc - 1) / rc, 0, 0, (long long)m * bb, false, st));
         return 0;
     }
     QF_HIP(qfec::launch_gf_encode(d_data, d_par, tab, k, m, bb, G, rc, st));
@@ -265,16 +272,15 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc, rmax,
                                     G, st));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
-    if (qfec::gf_ring_supported(k, m, bb, rc, nchunk)) {
-        // streams each group once and stores its recovered blocks after the group's last
-        // block is in LDS, so in place needs no scratch
+    if (qfec::gf_group_supported(k, m, bb, rc)) {
+        // whole group in LDS before any store: in place needs no scratch
         const int rcp = std::max(rc, 4);
-        QF_HIP(qfec::launch_gf_ring(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
-                                    nchunk, rmax, (long long)nchunk * k * rcp,
-                                    (long long)k * bb, true, st));
+        QF_HIP(qfec::launch_gf_group(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
+                                     nchunk, rmax, (long long)nchunk * k * rcp,
+                                     (long long)k * bb, true, st));
         return 0;
     }
-    if (nchunk > 1 && d_out == d_blocks && !qfec::gf_staged(d_blocks, k, bb, nchunk, rc)) {
+    if (nchunk > 1 && d_out == d_blocks) {
         // in place with several output chunks: a later chunk would read slots an earlier
         // chunk already overwrote, so stage the recovered blocks first
         QF_HIP(c->dscratch.ensure((size_t)G * rmax * bb));

@@ -61,25 +61,6 @@ hipError_t launch_gf_decode_scratch(const uint8_t* blocks, uint8_t* scratch, Dec
 hipError_t launch_scatter_recovered(const uint8_t* scratch, uint8_t* out, DecodeWork w, int k,
                                    int bb, int rmax, long long groups, hipStream_t st);
 
-// Streaming LDS-ring GF apply (gf_ring.hip): encode (coef shared, coef_gstride 0) or
-// decode (per-group coef, slots, nout).  No alignment requirement on `in`.
-struct RingArgs {
-    const uint8_t* in;
-    uint8_t* out;
-    const uint8_t* coef;
-    const uint8_t* slots;
-    const int32_t* nout;
-    long long groups, in_gstride, coef_gstride, out_gstride;
-    int k, m, bb, s, nw, ntiles, nchunk, rmax, nwaves;
-    int slot_bytes, team_bytes;
-};
-bool gf_ring_supported(int k, int m, int bb, int rc, int nchunk);
-hipError_t launch_gf_ring(const uint8_t* in, uint8_t* out, const uint8_t* coef,
-                          const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
-                          long long groups, int rc, int nchunk, int rmax,
-                          long long coef_gstride, long long out_gstride, bool decode,
-                          hipStream_t st);
-
 // m = 1 LDS-ring XOR kernel (xor_dma.hip).  Requires 16-byte aligned `in`, 8-byte aligned
 // `out`/stride and bb % 8 == 0; decode with rows_in != null also does the row bookkeeping.
 bool xor_dma_ok(const void* in, const void* out, int k, int bb, long long ogs);
@@ -88,8 +69,14 @@ hipError_t launch_xor_dma(const uint8_t* in, uint8_t* out, const uint8_t* eidx,
                           int bb, long long groups, long long out_gstride, bool decode,
                           hipStream_t st);
 
-// Whether a decode of this shape runs the LDS-staged kernel (no in-place hazard).
-bool gf_staged(const void* in, int k, int bb, int nchunk, int rc);
+// Whole-group LDS kernel for groups that fit in LDS (gf_group.hip).
+bool gf_group_supported(int k, int m, int bb, int rc);
+hipError_t launch_gf_group(const uint8_t* in, uint8_t* out, const uint8_t* coef,
+                           const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
+                           long long groups, int rc, int nchunk, int rmax,
+                           long long coef_gstride, long long out_gstride, bool decode,
+                           hipStream_t st);
+
 
 // Synthetic workload helpers (bench / tests): splitmix64 stream and receive-set gather.
 hipError_t launch_synth_fill(uint8_t* dst, unsigned long long bytes, unsigned long long seed,

@@ -245,14 +245,14 @@ __device__ __forceinline__ void store_word(uint8_t* sub, int c, const ColAccess&
 
 // Workgroup-size bound per output-chunk width: it caps VGPRs at 512 / ceil(waves / 4), so
 // the RC x 8 accumulators never spill (RC 4: 128 VGPR, RC 8: 170, RC 16: 256).
-template <int RC> struct StageBound { static constexpr int T = RC <= 4 ? 1024 : (RC == 8 ? 640 : 320); };
+template <int RC> struct ApplyBound { static constexpr int T = RC <= 4 ? 1024 : (RC == 8 ? 640 : 320); };
 
 // One wave = one (group, output chunk, 64-word column tile).  RC outputs per wave.
 //   coef:  [(g) * coef_gstride + (chunk * k + pos) * RCP + j]  (RCP = max(4, RC))
 //   encode: outputs o = chunk*RC + j < m go to out + g*out_gstride + o*bb
 //   decode: outputs o < nout[g] go to out + g*out_gstride + slots[g*rmax + o]*bb
 template <int RC, bool DECODE, bool TINY, int PD>
-__global__ __launch_bounds__(StageBound<RC>::T) void gf_apply_kernel(
+__global__ __launch_bounds__(ApplyBound<RC>::T) void gf_apply_kernel(
     const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, int k, int m, int bb,
     int nw, int ntiles, int nchunk, int rmax, long long coef_gstride, long long out_gstride,
@@ -342,177 +342,54 @@ __global__ __launch_bounds__(StageBound<RC>::T) void gf_apply_kernel(
     }
 }
 
-// LDS-staged variant (shipped for m > 1 whenever a group is 16-byte aligned): one
-// workgroup per group; waves = column tiles x output chunks, all reading the same staged
-// blocks.  Wave 0 streams block x + NSLOT - 1 into a ring of NSLOT block slots with
-// global_load_lds_dwordx4 nt (the DMA window starts at the 16-byte boundary at or below
-// the block, so no lane straddles the group end), and one workgroup barrier per block
-// both publishes the landed block and frees the slot of block x - 1.  The block's
-// sub-row words are read from LDS with unaligned ds_read_b32.  Every global read of the
-// group completes before any output is stored, so in-place decode needs no staging
-// copy even when the outputs span several chunks.
-__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
-    switch (n) {
-#define QF_W(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-        QF_W(0) QF_W(1) QF_W(2) QF_W(3) QF_W(4) QF_W(5) QF_W(6) QF_W(7) QF_W(8) QF_W(9)
-        QF_W(10) QF_W(11) QF_W(12) QF_W(13) QF_W(14) QF_W(15) QF_W(16) QF_W(17) QF_W(18)
-        QF_W(19) QF_W(20) QF_W(21) QF_W(22) QF_W(23) QF_W(24) QF_W(25) QF_W(26) QF_W(27)
-        QF_W(28) QF_W(29) QF_W(30) QF_W(31) QF_W(32) QF_W(33) QF_W(34) QF_W(35) QF_W(36)
-#undef QF_W
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-}
-
-constexpr int kStageSlots = 4;   // ring depth: 3 blocks in flight while one is combined
-
-
-template <int RC, bool DECODE>
-__global__ __launch_bounds__(StageBound<RC>::T) void gf_stage_kernel(
-    const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ coef,
-    const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, int k, int m, int bb,
-    int nw, int ntiles, int nchunk, int rmax, int npc, long long coef_gstride,
-    long long out_gstride) {
-    constexpr int RCP = RC < 4 ? 4 : RC;
-    constexpr int NCW = RCP / 4;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = threadIdx.x & 63;
-    const int w = wave_id();
-    const int nwaves = ntiles * nchunk;
-    const int tile = w % ntiles;
-    const int chunk = w / ntiles;
-    const long long g = blockIdx.x;
-    const int s = bb >> 3;
-    const int SB = npc * 1024;
-    const long long gb = (long long)k * bb;
-    const uint8_t* gin = in + g * gb;
-    int n = DECODE ? nout[g] : m;
-    n = min(n - chunk * RC, RC);
-    const int c = tile * 64 + lane;
-    const ColAccess ca = col_access<false>(c, nw, s);
-    if (DECODE && __builtin_amdgcn_readfirstlane(nout[g]) == 0) return;   // whole group idle
-
-    // This group's coefficient table ([nchunk][k][RCP] bytes) goes to LDS once, so the
-    // per-block coefficient fetch is an LDS broadcast, not a dependent global load.
-    uint32_t* lcoef = (uint32_t*)(smem + kStageSlots * SB);
-    {
-        const uint32_t* src = (const uint32_t*)(coef + g * coef_gstride);
-        const int nwords = nchunk * k * NCW;
-        for (int i = threadIdx.x; i < nwords; i += blockDim.x) lcoef[i] = src[i];
-    }
-
-    // DMA of block x: the 16-byte-aligned window [a0, a1) around the block, npc pieces of
-    // 1 KiB.  Lanes past a1 are masked; lane 0 always stays active (clamped into the
-    // window) so every piece is issued and the vmcnt arithmetic stays exact.
-    auto issue = [&](int x) {
-        const long long a0 = ((long long)x * bb) & ~15ll;
-        const long long a1 = (((long long)(x + 1) * bb) + 15) & ~15ll;
-        uint8_t* dst = smem + (x % kStageSlots) * SB;
-        for (int p = 0; p < npc; ++p) {
-            long long off = a0 + p * 1024 + lane * 16;
-            const bool act = off < a1;
-            if (!act) off = a1 - 16;
-            if (act || lane == 0)
-                __builtin_amdgcn_global_load_lds(QF_GPTR(gin + off), QF_LPTR(dst + p * 1024), 16,
-                                                 0, 2);
-        }
-    };
-    __syncthreads();   // lcoef visible (its fence drains only the coefficient loads)
-    constexpr int A = kStageSlots - 1;
-    if (w == 0)
-        for (int x = 0; x < A && x < k; ++x) issue(x);
-
-    uint32_t acc[RC][8];
-#pragma unroll
-    for (int j = 0; j < RC; ++j)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) acc[j][r] = 0;
-
-#pragma unroll 1
-    for (int x = 0; x < k; ++x) {
-        if (w == 0) {
-            const int issued = min(k, x + A);
-            wait_vmcnt_dyn(issued - x - 1 == A - 1 ? (A - 1) * npc : 0);
-        }
-        if (nwaves > 1) {
-            // raw barrier: __syncthreads() would emit vmcnt(0) and drain the DMA pipeline.
-            // Wave 0's counted wait above retired block x; the barrier publishes it to the
-            // other waves and proves block x - 1's slot is no longer being read.
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-        }
-        if (w == 0 && x + A < k) issue(x + A);
-        if (n > 0) {
-            uint32_t cwv[NCW];
-#pragma unroll
-            for (int q = 0; q < NCW; ++q)
-                cwv[q] = __builtin_amdgcn_readfirstlane(lcoef[(chunk * k + x) * NCW + q]);
-            const uint8_t* blk = smem + (x % kStageSlots) * SB + (((long long)x * bb) & 15) + ca.lo;
-            WZ v;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) v.W[t] = (*(const u32ua*)(blk + t * s)) >> ca.shift;
-            expand_wz(v);
-#pragma unroll
-            for (int j = 0; j < RC; ++j) {
-                if (j < n) {
-                    const uint32_t a = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-                    apply_nibble<0>(acc[j], a & 15u, v);
-                    apply_nibble<4>(acc[j], a >> 4, v);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < RC; ++j) {
-        if (j < n) {
-            const int o = chunk * RC + j;
-            const int slot = (DECODE && slots) ? slots[g * rmax + o] : o;
-            uint8_t* dst = out + g * out_gstride + (long long)slot * bb;
-#pragma unroll
-            for (int r = 0; r < 8; ++r) store_word(dst + r * s, c, ca, acc[j][r]);
-        }
-    }
-}
-
 // ------------------------------------------------------------------- decode prep
-// One 64-lane workgroup per group.  Restates the reference's decode bookkeeping
-// (sort_blocks :543-575, erasure list, recovery row rewrite :791) and replaces its GF(2)
-// bitmatrix elimination by a GF(256) Gauss-Jordan inverse of the r x r erasure submatrix
-// S[i][j] = C[y_i][e_j]: since c -> (8x8 expansion) is a ring homomorphism, the inverse
-// bitmatrix is the expansion of S^-1, and the recovered data is unique.  Output rows:
+// One wave per group (persistent: each wave walks groups w, w + W, ...; the GF log/exp
+// tables are staged in LDS once per workgroup).  Restates the reference's decode
+// bookkeeping (sort_blocks :543-575, erasure list, recovery row rewrite :791) and replaces
+// its GF(2) bitmatrix elimination by a GF(256) Gauss-Jordan inverse of the r x r erasure
+// submatrix S[i][j] = C[y_i][e_j]: since c -> (8x8 expansion) is a ring homomorphism, the
+// inverse bitmatrix is the expansion of S^-1, and the recovered data is unique.  Output:
 //   recovered e_j = sum_i Sinv[j][i] * R_i + sum_{x present} (sum_i Sinv[j][i] C[y_i][x]) * D_x
 // so one coefficient per (j, input slot) and a single pass over the received blocks.
-__global__ __launch_bounds__(64) void decode_prep_kernel(
-    const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
-    const uint8_t* __restrict__ cenc, uint8_t* __restrict__ coef, uint8_t* __restrict__ slots,
-    int32_t* __restrict__ nout, int k, int m, int bb, int rc, int rmax, int nchunk) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* gexp = smem;              // 512
-    uint8_t* glog = gexp + 512;        // 256
-    uint8_t* rowl = glog + 256;        // 256
-    uint8_t* present = rowl + 256;     // 256
-    uint8_t* recpos = present + 256;   // 256: slot of recovery i
-    uint8_t* era = recpos + 256;       // 256: erased row j
-    uint8_t* recidx = era + 256;       // 256: recovery index of slot (255 = original)
-    uint8_t* mat = recidx + 256;       // rmax x (2 rmax)
-    const int lane = threadIdx.x;
-    const long long g = blockIdx.x;
-    const int rcp = rc < 4 ? 4 : rc;
+// Lanes of one wave exchange data through LDS without barriers: a wave's LDS operations
+// execute in order, so wave_sync() only has to stop the compiler from reordering them.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
 
-    for (int i = lane; i < 512; i += 64) gexp[i] = c_gf.exp[i];
+struct PrepScratch {
+    uint8_t* rowl;      // 256
+    uint8_t* present;   // 256
+    uint8_t* recpos;    // 256: slot of recovery i
+    uint8_t* era;       // 256: erased row j
+    uint8_t* recidx;    // 256: recovery index of slot (255 = original)
+    uint8_t* mat;       // rmax x (2 rmax)
+};
+
+__device__ __forceinline__ void prep_group(
+    long long g, int lane, const uint8_t* gexp, const uint8_t* glog, const PrepScratch& sc,
+    const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
+    const uint8_t* cenc, uint8_t* __restrict__ coef, uint8_t* __restrict__ slots,
+    int32_t* __restrict__ nout, int k, int m, int bb, int rc, int rmax, int nchunk) {
+    uint8_t* rowl = sc.rowl;
+    uint8_t* present = sc.present;
+    uint8_t* recpos = sc.recpos;
+    uint8_t* era = sc.era;
+    uint8_t* recidx = sc.recidx;
+    uint8_t* mat = sc.mat;
+    const int rcp = rc < 4 ? 4 : rc;
     for (int i = lane; i < 256; i += 64) {
-        glog[i] = c_gf.log[i];
         present[i] = 0;
         recidx[i] = 255;
     }
     const uint8_t* rg = rows_in + g * k;
     uint8_t* ro = rows_out + g * k;
     for (int i = lane; i < k; i += 64) rowl[i] = rg[i];
-    __syncthreads();
+    wave_sync();
     for (int i = lane; i < k; i += 64)
         if (rowl[i] < k) present[rowl[i]] = 1;
-    __syncthreads();
-
+    wave_sync();
     // recovery blocks in array order (sort_blocks)
     int nrec = 0;
     for (int base = 0; base < k; base += 64) {
@@ -536,7 +413,7 @@ __global__ __launch_bounds__(64) void decode_prep_kernel(
         if (miss && nera + pre < nrec) era[nera + pre] = (uint8_t)x;
         nera += __popcll(msk);
     }
-    __syncthreads();
+    wave_sync();
 
     auto finish_unchanged = [&](int st) {
         if (ro != rg)
@@ -564,7 +441,7 @@ __global__ __launch_bounds__(64) void decode_prep_kernel(
         else v = (j - n == i) ? 1 : 0;
         mat[i * n2 + j] = v;
     }
-    __syncthreads();
+    wave_sync();
     auto mul = [&](uint8_t a, uint8_t b) -> uint8_t {
         return (a && b) ? gexp[glog[a] + glog[b]] : 0;
     };
@@ -582,19 +459,19 @@ __global__ __launch_bounds__(64) void decode_prep_kernel(
                 mat[p * n2 + j] = mat[piv * n2 + j];
                 mat[piv * n2 + j] = t;
             }
-            __syncthreads();
+            wave_sync();
         }
         const uint8_t inv = gexp[255 - glog[mat[p * n2 + p]]];
-        __syncthreads();
+        wave_sync();
         for (int j = lane; j < n2; j += 64) mat[p * n2 + j] = mul(mat[p * n2 + j], inv);
-        __syncthreads();
+        wave_sync();
         for (int i = 0; i < n; ++i) {
             if (i == p) continue;
             const uint8_t f = mat[i * n2 + p];
-            __syncthreads();
+            wave_sync();
             if (f)
                 for (int j = lane; j < n2; j += 64) mat[i * n2 + j] ^= mul(f, mat[p * n2 + j]);
-            __syncthreads();
+            wave_sync();
         }
     }
 
@@ -618,7 +495,7 @@ __global__ __launch_bounds__(64) void decode_prep_kernel(
     }
     if (ro != rg)
         for (int i = lane; i < k; i += 64) ro[i] = rowl[i];
-    __syncthreads();
+    wave_sync();
     for (int j = lane; j < n; j += 64) {
         slots[g * rmax + j] = recpos[j];
         ro[recpos[j]] = era[j];                                            // :791
@@ -627,6 +504,30 @@ __global__ __launch_bounds__(64) void decode_prep_kernel(
         nout[g] = n;
         if (status) status[g] = 0;
     }
+}
+
+__global__ __launch_bounds__(256) void decode_prep_kernel(
+    const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
+    const uint8_t* __restrict__ cenc, uint8_t* __restrict__ coef, uint8_t* __restrict__ slots,
+    int32_t* __restrict__ nout, long long groups, int k, int m, int bb, int rc, int rmax,
+    int nchunk, int scratch_bytes) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* gexp = smem;              // 512
+    uint8_t* glog = gexp + 512;        // 256
+    uint8_t* lcenc = glog + 256;       // m x k encode matrix (the inner loops read it at random)
+    const int cbytes = (m * k + 15) & ~15;
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) gexp[i] = c_gf.exp[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) glog[i] = c_gf.log[i];
+    for (int i = threadIdx.x; i < m * k; i += blockDim.x) lcenc[i] = cenc[i];
+    __syncthreads();
+    const int nwv = blockDim.x >> 6;
+    const int w = wave_id(), lane = threadIdx.x & 63;
+    uint8_t* base = lcenc + cbytes + (size_t)w * scratch_bytes;
+    PrepScratch sc{base, base + 256, base + 512, base + 768, base + 1024, base + 1280};
+    for (long long g = (long long)blockIdx.x * nwv + w; g < groups;
+         g += (long long)gridDim.x * nwv)
+        prep_group(g, lane, gexp, glog, sc, rows_in, rows_out, status, lcenc, coef, slots, nout,
+                   k, m, bb, rc, rmax, nchunk);
 }
 
 // In-place decode with more recovered blocks than one wave holds: the chunks write to a
@@ -790,18 +691,6 @@ static int pd_choice() {
     return pd;
 }
 
-// The LDS-staged GF kernel is opt-in (QFEC_STAGE=1): on MI355X it measured 2x slower
-// than the register-pipelined gf_apply_kernel on both (32, 4, 1352) and (128, 16, 9008)
-// (profiles/r01/README.md).
-static bool stage_disabled() {
-    static int d = -1;
-    if (d < 0) {
-        const char* e = getenv("QFEC_STAGE");
-        d = e && atoi(e) ? 0 : 1;
-    }
-    return d;
-}
-
 template <bool DECODE>
 static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8_t* coef,
                                     const uint8_t* slots, const int32_t* nout, int k, int m,
@@ -814,30 +703,6 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
     const long long units = groups * nchunk * ntiles;
     if (units <= 0) return hipSuccess;
     if (units > 0x7fffffffLL) return hipErrorInvalidValue;
-    const long long gb = (long long)k * bb;
-    const int npc = (int)((15 + bb + 1023) / 1024);
-    const int rcp = rc < 4 ? 4 : rc;
-    // ring of block slots + this group's coefficient table
-    const size_t lds = (size_t)kStageSlots * npc * 1024 + (((size_t)nchunk * k * rcp + 15) & ~15ull);
-    const int maxt = rc <= 4 ? 1024 : (rc == 8 ? 640 : 320);
-    if (!stage_disabled() && s >= 4 && gb % 16 == 0 && ((uintptr_t)in & 15) == 0 &&
-        ntiles * nchunk * 64 <= maxt && lds <= 64 * 1024 && groups <= 0x7fffffffLL) {
-        const unsigned nthreads = (unsigned)(ntiles * nchunk * 64);
-#define QF_STAGE(RCV)                                                                         \
-    gf_stage_kernel<RCV, DECODE><<<(unsigned)groups, nthreads, lds, st>>>(                    \
-        in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, npc, coef_gstride,    \
-        out_gstride)
-        switch (rc) {
-            case 1: QF_STAGE(1); break;
-            case 2: QF_STAGE(2); break;
-            case 4: QF_STAGE(4); break;
-            case 8: QF_STAGE(8); break;
-            case 16: QF_STAGE(16); break;
-            default: return hipErrorInvalidValue;
-        }
-#undef QF_STAGE
-        return hipGetLastError();
-    }
     const int per_group = nchunk * ntiles;
     const unsigned nb = blocks_for_waves(units);
     const unsigned nthr = 256;
@@ -874,21 +739,6 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
     return hipGetLastError();
 }
 
-// True when gf_apply_dispatch will take the staged path (in-place decode then needs no
-// scratch even with several output chunks).
-bool gf_staged(const void* in, int k, int bb, int nchunk, int rc) {
-    const int s = bb / 8;
-    const int nw = (s + 3) / 4;
-    const int ntiles = (nw + 63) / 64;
-    const long long gb = (long long)k * bb;
-    const int npc = (int)((15 + bb + 1023) / 1024);
-    const int maxt = rc <= 4 ? 1024 : (rc == 8 ? 640 : 320);
-    const size_t lds = (size_t)kStageSlots * npc * 1024 +
-                       (((size_t)nchunk * k * (rc < 4 ? 4 : rc) + 15) & ~15ull);
-    return !stage_disabled() && s >= 4 && gb % 16 == 0 && ((uintptr_t)in & 15) == 0 &&
-           ntiles * nchunk * 64 <= maxt && lds <= 64 * 1024;
-}
-
 hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t* coef, int k,
                             int m, int bb, long long groups, int rc, hipStream_t st) {
     const int nchunk = (m + rc - 1) / rc;
@@ -900,12 +750,17 @@ hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t
                               const uint8_t* cenc, DecodeWork w, int k, int m, int bb, int rc,
                               int rmax, long long groups, hipStream_t st) {
     if (groups <= 0) return hipSuccess;
-    if (groups > 0x7fffffffLL) return hipErrorInvalidValue;
     const int nchunk = (rmax + rc - 1) / rc;
-    const size_t lds = 512 + 256 * 6 + (size_t)rmax * 2 * rmax;
-    decode_prep_kernel<<<(unsigned)groups, 64, lds, st>>>(rows_in, rows_out, status, cenc,
-                                                          w.coef, w.slots, w.nout, k, m, bb,
-                                                          rc, rmax, nchunk);
+    const int scratch = (int)((1280 + (size_t)rmax * 2 * rmax + 15) & ~(size_t)15);
+    const size_t fixed = 768 + (((size_t)m * k + 15) & ~(size_t)15);
+    int nwv = 4;
+    while (nwv > 1 && fixed + (size_t)nwv * scratch > 64 * 1024) nwv >>= 1;
+    const size_t lds = fixed + (size_t)nwv * scratch;
+    const long long want = (groups + nwv - 1) / nwv;
+    const unsigned nb = (unsigned)std::min<long long>(want, (long long)num_cus() * 16);
+    decode_prep_kernel<<<nb, nwv * 64, lds, st>>>(rows_in, rows_out, status, cenc, w.coef,
+                                                   w.slots, w.nout, groups, k, m, bb, rc, rmax,
+                                                   nchunk, scratch);
     return hipGetLastError();
 }
 
