@@ -86,11 +86,11 @@ __global__ __launch_bounds__(256) void reg_aligned(const uint8_t* __restrict__ i
 }
 
 // (c) per-wave LDS ring of NS block windows via LDS-DMA, one group per wave
-template <int NS>
+template <int NS, bool CLAMP = false, int WPB = 4>
 __global__ __launch_bounds__(256) void lds_ring(const uint8_t* __restrict__ in, uint8_t* out, long long G) {
-    constexpr int SLOT = 1376;
+    constexpr int SLOT = CLAMP ? 2048 : 1376;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const long long g = (long long)blockIdx.x * 4 + wid();
+    const long long g = (long long)blockIdx.x * WPB + wid();
     if (g >= G) return;
     const int lane = threadIdx.x & 63;
     const int w = wid();
@@ -103,7 +103,14 @@ __global__ __launch_bounds__(256) void lds_ring(const uint8_t* __restrict__ in, 
         const int U = (int)(((b + BB + 15) & ~(uintptr_t)15) - b0) >> 4;
         uint8_t* sl = ring + (x % NS) * SLOT;
         __builtin_amdgcn_global_load_lds(GPTR(b0 + lane * 16), LPTR(sl), 16, 0, 2);
-        if (64 + lane < U) __builtin_amdgcn_global_load_lds(GPTR(b0 + 1024 + lane * 16), LPTR(sl + 1024), 16, 0, 2);
+        if (CLAMP) {
+            // all lanes active: lanes past the window re-load its last 16 B into the
+            // slot's padding (slot = 2 KiB)
+            const int u = min(64 + lane, U - 1);
+            __builtin_amdgcn_global_load_lds(GPTR(b0 + u * 16), LPTR(sl + 1024), 16, 0, 2);
+        } else if (64 + lane < U) {
+            __builtin_amdgcn_global_load_lds(GPTR(b0 + 1024 + lane * 16), LPTR(sl + 1024), 16, 0, 2);
+        }
     };
     uint32_t acc[8] = {0};
 #pragma unroll
@@ -183,6 +190,10 @@ int main() {
     timeit("c lds_ring NS4", [&] { hipLaunchKernelGGL(lds_ring<4>, dim3(nb4), dim3(256), 4 * 4 * 1376, 0, in, out, G); }, bytes, reps);
     timeit("c lds_ring NS6", [&] { hipLaunchKernelGGL(lds_ring<6>, dim3(nb4), dim3(256), 4 * 6 * 1376, 0, in, out, G); }, bytes, reps);
     timeit("c lds_ring NS8", [&] { hipLaunchKernelGGL(lds_ring<8>, dim3(nb4), dim3(256), 4 * 8 * 1376, 0, in, out, G); }, bytes, reps);
+    timeit("c lds_ring NS4 clamp", [&] { hipLaunchKernelGGL((lds_ring<4, true>), dim3(nb4), dim3(256), 4 * 4 * 2048, 0, in, out, G); }, bytes, reps);
+    timeit("c lds_ring NS8 clamp", [&] { hipLaunchKernelGGL((lds_ring<8, true>), dim3(nb4), dim3(256), 4 * 8 * 2048, 0, in, out, G); }, bytes, reps);
+    timeit("c lds_ring NS8 clamp 1w", [&] { hipLaunchKernelGGL((lds_ring<8, true, 1>), dim3((unsigned)G), dim3(64), 8 * 2048, 0, in, out, G); }, bytes, reps);
+    timeit("c lds_ring NS16 clamp 1w", [&] { hipLaunchKernelGGL((lds_ring<16, true, 1>), dim3((unsigned)G), dim3(64), 16 * 2048, 0, in, out, G); }, bytes, reps);
     timeit("d lds_group 1w", [&] { hipLaunchKernelGGL(lds_group, dim3((unsigned)G), dim3(64), 44 * 1024, 0, in, out, G); }, bytes, reps);
     timeit("d lds_group 3w", [&] { hipLaunchKernelGGL(lds_group, dim3((unsigned)((G + 2) / 3)), dim3(192), 3 * 44 * 1024, 0, in, out, G); }, bytes, reps);
     return 0;
