@@ -123,7 +123,7 @@ def pmc_traffic(workload, phase, groups):
     return round(tot * groups / d["groups"]), os.path.relpath(files[-1], ROOT)
 
 
-def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps):
+def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps, recovered):
     """Host-resident rate: pinned host buffers in and out, H2D + kernels + D2H through the
     library's pipelined host-pointer entry points (qfec_*_batch_host).  Never `value`."""
     import torch
@@ -138,6 +138,9 @@ def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps):
     blocks_h = torch.empty_like(blocks0).pin_memory()
     rows_h = torch.empty_like(rows0).pin_memory()
     status_h = torch.zeros((G,), dtype=torch.int32).pin_memory()
+    rmax = min(k, m)
+    rec_h = torch.empty((G, rmax, bb), dtype=torch.uint8, pin_memory=True)
+    rec_rows_h = torch.empty((G, rmax), dtype=torch.uint8, pin_memory=True)
     t_enc = t_dec = 0.0
     for i in range(steps + 1):
         blocks_h.copy_(blocks0)
@@ -145,13 +148,20 @@ def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps):
         t0 = time.perf_counter()
         fec.encode_host_into(eng, k, m, bb, data_h, parity_h)
         t1 = time.perf_counter()
-        fec.decode_host_into(eng, k, m, bb, blocks_h, rows_h, status_h)
+        if recovered:
+            fec.decode_recovered_host_into(eng, k, m, bb, blocks_h, rows_h, rec_h, rec_rows_h,
+                                           status_h)
+        else:
+            fec.decode_host_into(eng, k, m, bb, blocks_h, rows_h, status_h)
         t2 = time.perf_counter()
         if i:                      # first pass warms the staging buffers
             t_enc += t1 - t0
             t_dec += t2 - t1
     ok = int(status_h.abs().max()) == 0
-    pcie = G * (k * bb + m * bb) + G * (2 * k * bb + 2 * k + 4)
+    if recovered:
+        pcie = G * (k * bb + m * bb) + G * (k * bb + k + rmax * bb + rmax + 4)
+    else:
+        pcie = G * (k * bb + m * bb) + G * (2 * k * bb + 2 * k + 4)
     return {
         "value": round(G * k * payload / 2**30 / ((t_enc + t_dec) / steps), 3),
         "unit": "GiB/s",
@@ -160,9 +170,10 @@ def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps):
         "pcie_bytes_per_step": pcie,
         "pcie_GBps": round(pcie / ((t_enc + t_dec) / steps) / 1e9, 2),
         "status_ok": ok,
-        "note": "pinned host buffers; qfec_encode_batch_host + qfec_decode_batch_host "
-                "(in place, cauchy_256_decode semantics), 64 MiB chunks, H2D/kernel/D2H "
-                "pipelined; not the bench value",
+        "note": "pinned host buffers; qfec_encode_batch_host + "
+                + ("qfec_decode_batch_recovered_host (recovered blocks only)" if recovered
+                   else "qfec_decode_batch_host (in place, cauchy_256_decode semantics)")
+                + ", 64 MiB chunks, H2D/kernel/D2H pipelined; not the bench value",
     }
 
 
@@ -178,6 +189,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check recovered data after timing")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) leg")
+    ap.add_argument("--decode-layout", default="recovered", choices=["recovered", "slots"],
+                    help="recovered: qfec_decode_batch_recovered writes the r recovered blocks "
+                         "of each group densely (what the receiver consumes); slots: "
+                         "qfec_decode_batch writes them into their slots of a [G][k][bb] "
+                         "buffer (cauchy_256_decode layout, out of place)")
     ap.add_argument("--host-steps", type=int, default=3)
     args = ap.parse_args()
 
@@ -218,8 +234,14 @@ def main():
     src = torch.from_numpy(src_np).to(dev)
     blocks = torch.empty((G, k, bb), dtype=torch.uint8, device=dev)
     fec.synth_gather(data, parity, src, blocks, k, m, bb)
-    out = torch.zeros_like(blocks)
-    rows_out = torch.zeros_like(rows)
+    rmax = min(k, m)
+    recovered = args.decode_layout == "recovered"
+    if recovered:
+        out = torch.zeros((G, rmax, bb), dtype=torch.uint8, device=dev)
+        rows_out = torch.zeros((G, rmax), dtype=torch.uint8, device=dev)
+    else:
+        out = torch.zeros_like(blocks)
+        rows_out = torch.zeros_like(rows)
     status = torch.zeros((G,), dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
 
@@ -229,7 +251,10 @@ def main():
         eng.encode(k, m, bb, data, parity)
         if ev is not None:
             ev[1].record(stream)
-        eng.decode(k, m, bb, blocks, rows, out=out, rows_out=rows_out, status=status)
+        if recovered:
+            eng.decode_recovered(k, m, bb, blocks, rows, out, rows_out, status=status)
+        else:
+            eng.decode(k, m, bb, blocks, rows, out=out, rows_out=rows_out, status=status)
         if ev is not None:
             ev[2].record(stream)
 
@@ -271,17 +296,24 @@ def main():
         phase = "decode"
     traffic, traffic_src = pmc_traffic(args.workload, phase, G)
     if enc_ms >= dec_ms:
-        dom = ("encode", "xor_encode_kernel" if m == 1 else "gf_apply_kernel<encode>",
+        dom = ("encode", "xor_dma_kernel<encode>" if m == 1 else "gf_apply_kernel<encode>",
                enc_gbs, enc_bytes)
     else:
-        dom = ("decode", "xor_decode_kernel" if m == 1 else "decode_prep + gf_apply<decode>",
-               dec_gbs, dec_bytes)
+        dom = ("decode", "xor_dma_kernel<decode>" if m == 1
+               else "decode_prep_kernel + gf_apply_kernel<decode>", dec_gbs, dec_bytes)
 
     verified = None
     if args.verify:
-        slot = rows.long() >= k
-        g_idx = torch.arange(G, device=dev)[:, None].expand(G, k)[slot]
-        verified = bool(torch.equal(out[slot], data[g_idx, rows_out.long()[slot]]))
+        if recovered:
+            # every group recovered exactly r blocks, each equal to the data row it names
+            got = rows_out != 255
+            g_idx = torch.arange(G, device=dev)[:, None].expand(G, rmax)[got]
+            verified = bool((got.sum(dim=1) == r).all()) and bool(
+                torch.equal(out[got], data[g_idx, rows_out.long()[got]]))
+        else:
+            slot = rows.long() >= k
+            g_idx = torch.arange(G, device=dev)[:, None].expand(G, k)[slot]
+            verified = bool(torch.equal(out[slot], data[g_idx, rows_out.long()[slot]]))
         verified = verified and int(status.abs().max()) == 0
 
     cpu = None
@@ -292,7 +324,8 @@ def main():
 
     host = None
     if rank == 0 and world == 1 and not args.no_host:
-        host = host_inclusive(eng, k, m, bb, payload, data, blocks, rows, args.host_steps)
+        host = host_inclusive(eng, k, m, bb, payload, data, blocks, rows, args.host_steps,
+                              recovered)
 
     if rank == 0:
         line = {
@@ -316,6 +349,7 @@ def main():
                 "k": k, "m": m, "payload_bytes": payload, "block_bytes": bb,
                 "losses_per_group": r,
                 "parallelism": f"{world} independent group shards (no collective)",
+                "decode_layout": args.decode_layout,
             },
             "roofline": {
                 "bound": "hbm",

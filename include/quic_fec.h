@@ -85,12 +85,31 @@ QFEC_API int qfec_decode_batch(qfec_ctx *ctx, int k, int m, int block_bytes, lon
                       unsigned char *d_out, unsigned char *d_rows_out, int *d_status,
                       void *stream);
 
-/* Host-pointer variants: pinned staging, H2D, kernels, D2H; synchronous.  The decode
- * works in place on h_blocks / h_rows like cauchy_256_decode. */
+/* Receiver-side decode, recovered-blocks layout.  Same per-group decode as
+ * qfec_decode_batch, but d_blocks and d_rows_in are left untouched and only the recovered
+ * blocks are written, densely: with rmax = min(k, m), recovered block j of group g goes to
+ * d_rec + (g * rmax + j) * block_bytes and the data row it restores to
+ * d_rec_rows[g * rmax + j] -- ascending, the order cauchy_256_decode assigns them
+ * (cauchy_256.cpp:570-574) -- and 255 past the group's erasure count (the d_rec bytes of
+ * such entries are unspecified).  This is what QuicFecGroup::getRevivedPackets consumes
+ * (quic_fec_group.cc:280-293).  d_status may be NULL. */
+QFEC_API int qfec_decode_batch_recovered(qfec_ctx *ctx, int k, int m, int block_bytes,
+                                long long groups, const unsigned char *d_blocks,
+                                const unsigned char *d_rows_in, unsigned char *d_rec,
+                                unsigned char *d_rec_rows, int *d_status, void *stream);
+
+/* Host-pointer variants: H2D, kernels, D2H, chunked and pipelined; synchronous (pass
+ * pinned memory for full PCIe speed).  qfec_decode_batch_host works in place on h_blocks /
+ * h_rows like cauchy_256_decode; qfec_decode_batch_recovered_host returns only the
+ * recovered blocks, as qfec_decode_batch_recovered does. */
 QFEC_API int qfec_encode_batch_host(qfec_ctx *ctx, int k, int m, int block_bytes, long long groups,
                            const unsigned char *h_data, unsigned char *h_parity);
 QFEC_API int qfec_decode_batch_host(qfec_ctx *ctx, int k, int m, int block_bytes, long long groups,
                            unsigned char *h_blocks, unsigned char *h_rows, int *h_status);
+QFEC_API int qfec_decode_batch_recovered_host(qfec_ctx *ctx, int k, int m, int block_bytes,
+                                     long long groups, const unsigned char *h_blocks,
+                                     const unsigned char *h_rows, unsigned char *h_rec,
+                                     unsigned char *h_rec_rows, int *h_status);
 
 /* ---------------------------------------------------------------------------------
  * Support: the coefficient tables, a seeded synthetic workload, diagnostics.

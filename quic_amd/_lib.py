@@ -42,6 +42,16 @@ SIGNATURES = {
     "qfec_decode_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p]),
+    "qfec_decode_batch_recovered": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_int, ctypes.c_longlong,
+                                                   ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_void_p]),
+    "qfec_decode_batch_recovered_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
+                                                        ctypes.c_int, ctypes.c_int,
+                                                        ctypes.c_longlong, ctypes.c_void_p,
+                                                        ctypes.c_void_p, ctypes.c_void_p,
+                                                        ctypes.c_void_p, ctypes.c_void_p]),
     "qfec_cauchy_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "qfec_synth_fill": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_ulonglong, ctypes.c_ulonglong,
                                        ctypes.c_ulonglong, ctypes.c_void_p]),

@@ -294,6 +294,40 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     return 0;
 }
 
+// Recovered-blocks layout (qfec_decode_batch_recovered): the same decode, but recovered
+// block j of group g goes to d_rec + (g * rmax + j) * bb and its data row to
+// d_rec_rows[g * rmax + j] (ascending, 255 past the erasure count); blocks and row tags
+// are left as they are.  This is what the receiver consumes (getRevivedPackets,
+// quic_fec_group.cc:280-293, only extracts the missing packets), and the writes are dense.
+int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
+                          const uint8_t* d_blocks, const uint8_t* d_rows_in, uint8_t* d_rec,
+                          uint8_t* d_rec_rows, int32_t* d_status, hipStream_t st) {
+    if (G == 0) return 0;
+    const int rmax = std::min(k, m);
+    if (k <= 1) {
+        QF_HIP(qfec::launch_rec_k1(d_blocks, d_rows_in, d_rec, d_rec_rows, d_status, bb, rmax, G,
+                                   st));
+        return 0;
+    }
+    if (m == 1) {
+        QF_HIP(c->dslots.ensure((size_t)G));
+        QF_HIP(qfec::launch_xor_decode(d_blocks, d_rec, d_rows_in, d_rec_rows, d_status,
+                                       (uint8_t*)c->dslots.p, k, bb, G, st, true));
+        return 0;
+    }
+    const int rc = decode_rc(rmax);
+    const uint8_t* cenc = nullptr;
+    int r = get_cenc(c, k, m, &cenc);
+    if (r) return r;
+    if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
+    qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
+    QF_HIP(qfec::launch_decode_prep(d_rows_in, nullptr, d_status, cenc, w, k, m, bb, rc, rmax, G,
+                                    st, d_rec_rows));
+    if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
+    QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, d_rec, w, k, m, bb, G, rc, rmax, st));
+    return 0;
+}
+
 // Host-pointer batches, chunked and pipelined: chunk i's H2D (s_in), kernels (stream)
 // and D2H (s_out) are ordered by events, and NB staging buffers rotate, so the copy-in of
 // chunk i + 1 and the copy-out of chunk i - 1 overlap the kernels of chunk i (PCIe is
@@ -419,6 +453,62 @@ int qfec_decode_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
     if ((rc = set_device(c))) return rc;
     return decode_impl(c, k, m, bb, groups, d_blocks, d_rows_in, d_out, d_rows_out,
                        (int32_t*)d_status, pick(c, stream));
+}
+
+int qfec_decode_batch_recovered(qfec_ctx* c, int k, int m, int bb, long long groups,
+                                const unsigned char* d_blocks, const unsigned char* d_rows_in,
+                                unsigned char* d_rec, unsigned char* d_rec_rows, int* d_status,
+                                void* stream) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    if (groups && (!d_blocks || !d_rows_in || !d_rec || !d_rec_rows))
+        return fail(-2, "null buffer");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    return decode_recovered_impl(c, k, m, bb, groups, d_blocks, d_rows_in, d_rec, d_rec_rows,
+                                 (int32_t*)d_status, pick(c, stream));
+}
+
+int qfec_decode_batch_recovered_host(qfec_ctx* c, int k, int m, int bb, long long groups,
+                                     const unsigned char* h_blocks, const unsigned char* h_rows,
+                                     unsigned char* h_rec, unsigned char* h_rec_rows,
+                                     int* h_status) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    if (groups == 0) return 0;
+    if (!h_blocks || !h_rows || !h_rec || !h_rec_rows) return fail(-2, "null buffer");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    const int rmax = std::min(k, m);
+    const size_t blk_g = (size_t)k * bb, rec_g = (size_t)rmax * bb;
+    // per group: blocks, recovered blocks, row tags, recovered rows, status (aligned)
+    const size_t per = blk_g + rec_g + k + rmax + sizeof(int32_t);
+    return host_pipeline(c, groups, per, [&](long long g0, long long n, uint8_t* buf,
+                                             int phase) -> int {
+        uint8_t* db = buf;
+        uint8_t* dre = db + (size_t)n * blk_g;
+        uint8_t* dr = dre + (size_t)n * rec_g;
+        uint8_t* drr = dr + (size_t)n * k;
+        int32_t* ds = (int32_t*)(((uintptr_t)(drr + (size_t)n * rmax) + 3) & ~(uintptr_t)3);
+        if (phase == 0) {
+            QF_HIP(hipMemcpyAsync(db, h_blocks + (size_t)g0 * blk_g, (size_t)n * blk_g,
+                                  hipMemcpyHostToDevice, c->s_in));
+            QF_HIP(hipMemcpyAsync(dr, h_rows + (size_t)g0 * k, (size_t)n * k,
+                                  hipMemcpyHostToDevice, c->s_in));
+        } else if (phase == 1) {
+            const int r = decode_recovered_impl(c, k, m, bb, n, db, dr, dre, drr, ds, c->stream);
+            if (r) return r;
+        } else {
+            QF_HIP(hipMemcpyAsync(h_rec + (size_t)g0 * rec_g, dre, (size_t)n * rec_g,
+                                  hipMemcpyDeviceToHost, c->s_out));
+            QF_HIP(hipMemcpyAsync(h_rec_rows + (size_t)g0 * rmax, drr, (size_t)n * rmax,
+                                  hipMemcpyDeviceToHost, c->s_out));
+            if (h_status)
+                QF_HIP(hipMemcpyAsync(h_status + g0, ds, (size_t)n * sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, c->s_out));
+        }
+        return 0;
+    });
 }
 
 int qfec_encode_batch_host(qfec_ctx* c, int k, int m, int bb, long long groups,

@@ -25,14 +25,20 @@ hipError_t launch_xor_encode(const uint8_t* data, uint8_t* parity, int k, int bb
                              long long groups, long long out_gstride, hipStream_t st);
 
 // m == 1 decode: XOR the k-1 other blocks into the block tagged row >= k.  eidx is a
-// [G] byte workspace (erased slot per group).
+// [G] byte workspace (erased slot per group).  compact: the recovered block of group g
+// goes to out + g * bb and its data row to rows_out[g] (255 = nothing erased).
 hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t* rows_in,
                              uint8_t* rows_out, int32_t* status, uint8_t* eidx, int k, int bb,
-                             long long groups, hipStream_t st);
+                             long long groups, hipStream_t st, bool compact = false);
 
 // k <= 1 encode: copy data[0] into each of the m outputs (cauchy_256.cpp:1508-1516).
 hipError_t launch_replicate(const uint8_t* data, uint8_t* parity, int m, int bb,
                             long long groups, hipStream_t st);
+
+// k <= 1 decode in the recovered-blocks layout (rec [G][rmax][bb], rec_rows [G][rmax]).
+hipError_t launch_rec_k1(const uint8_t* blocks, const uint8_t* rows_in, uint8_t* rec,
+                        uint8_t* rec_rows, int32_t* status, int bb, int rmax, long long groups,
+                        hipStream_t st);
 
 // k <= 1 decode: row := 0 (cauchy_256.cpp:1257-1261).
 hipError_t launch_rows_k1(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
@@ -45,9 +51,12 @@ hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t*
 
 // Decode prep: per group, sort blocks, invert the erasure submatrix in GF(256) and
 // emit the r x k recovery coefficients.  cenc is the [m][k] encode matrix (row 0 = ones).
+// rows_out == nullptr: recovered-blocks layout, rec_rows [G][rmax] gets the data row of
+// recovered block j (ascending), 255 past the group's erasure count.
 hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
                               const uint8_t* cenc, DecodeWork w, int k, int m, int bb,
-                              int rc, int rmax, long long groups, hipStream_t st);
+                              int rc, int rmax, long long groups, hipStream_t st,
+                              uint8_t* rec_rows = nullptr);
 
 // Decode apply: recovered block j of group g = sum_pos coef[g][..][pos][j] (x) blocks[g][pos],
 // written to out[g][slots[g][j]].
@@ -64,10 +73,11 @@ hipError_t launch_scatter_recovered(const uint8_t* scratch, uint8_t* out, Decode
 // m = 1 LDS-ring XOR kernel (xor_dma.hip).  Requires 16-byte aligned `in`, 8-byte aligned
 // `out`/stride and bb % 8 == 0; decode with rows_in != null also does the row bookkeeping.
 bool xor_dma_ok(const void* in, const void* out, int k, int bb, long long ogs);
+// compact: recovered-blocks layout (out [G][bb], rows_out [G] = recovered data row).
 hipError_t launch_xor_dma(const uint8_t* in, uint8_t* out, const uint8_t* eidx,
                           const uint8_t* rows_in, uint8_t* rows_out, int32_t* status, int k,
                           int bb, long long groups, long long out_gstride, bool decode,
-                          hipStream_t st);
+                          hipStream_t st, bool compact = false);
 
 // Whole-group LDS kernel for groups that fit in LDS (gf_group.hip).
 bool gf_group_supported(int k, int m, int bb, int rc);

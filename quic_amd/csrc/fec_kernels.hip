@@ -71,7 +71,8 @@ template <> struct Unit<4> {
 template <int VS, int K, bool DECODE>
 __global__ __launch_bounds__(256) void xor_flat_kernel(
     const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ eidx, int k,
-    int bb, int nu, unsigned total_units, long long in_gstride, long long out_gstride) {
+    int bb, int nu, unsigned total_units, long long in_gstride, long long out_gstride,
+    long long e_stride) {
     typedef typename Unit<VS>::T V;
     const unsigned u = blockIdx.x * 256u + threadIdx.x;
     if (u >= total_units) return;
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(256) void xor_flat_kernel(
     uint8_t* dst = out + (long long)g * out_gstride;
     if (DECODE) {
         if (e == 255) return;   // nothing erased in this group
-        dst += (long long)e * bb;
+        dst += (long long)e * e_stride;   // e_stride 0: recovered-blocks layout
     }
     const int own = q * VS;   // first byte this unit owns
     if (own + VS <= bb) {
@@ -122,7 +123,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 template <bool DECODE>
 __global__ __launch_bounds__(256) void xor_bytes_kernel(
     const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ eidx, int k,
-    int bb, long long total, long long in_gstride, long long out_gstride) {
+    int bb, long long total, long long in_gstride, long long out_gstride, long long e_stride) {
     const long long u = (long long)blockIdx.x * 256 + threadIdx.x;
     if (u >= total) return;
     const long long g = u / bb;
@@ -134,23 +135,25 @@ __global__ __launch_bounds__(256) void xor_bytes_kernel(
     if (DECODE) {
         const int e = eidx[g];
         if (e == 255) return;
-        dst += (long long)e * bb;
+        dst += (long long)e * e_stride;
     }
     dst[i] = acc;
 }
 
 // m = 1 decode bookkeeping (cauchy_decode_m1, cauchy_256.cpp:486-540), one thread per
 // group: the erased slot is the first with row >= k; its new row is the first data row
-// not tagged by any other slot.  eidx[g] = that slot (255 = nothing erased).
+// not tagged by any other slot.  eidx[g] = that slot (255 = nothing erased).  compact:
+// rows_out is [G] and receives the recovered data row (255 = nothing erased) instead of
+// the rewritten tags.
 __global__ __launch_bounds__(256) void m1_prep_kernel(const uint8_t* __restrict__ rows_in,
                                                       uint8_t* rows_out,
                                                       int32_t* __restrict__ status,
                                                       uint8_t* __restrict__ eidx, int k,
-                                                      long long groups) {
+                                                      long long groups, int compact) {
     const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
     if (g >= groups) return;
     const uint8_t* rg = rows_in + g * k;
-    uint8_t* ro = rows_out + g * k;
+    uint8_t* ro = compact ? nullptr : rows_out + g * k;
     uint64_t seen[4] = {0, 0, 0, 0};
     int e = -1;
     for (int i = 0; i < k; ++i) {
@@ -159,11 +162,12 @@ __global__ __launch_bounds__(256) void m1_prep_kernel(const uint8_t* __restrict_
             if (e < 0) { e = i; continue; }
         }
         if (r < k) seen[r >> 6] |= 1ull << (r & 63);
-        if (ro != rg) ro[i] = (uint8_t)r;
+        if (ro && ro != rg) ro[i] = (uint8_t)r;
     }
     if (status) status[g] = 0;
     if (e < 0) {
         eidx[g] = 255;
+        if (compact) rows_out[g] = 255;
         return;
     }
     int miss = -1;
@@ -175,7 +179,9 @@ __global__ __launch_bounds__(256) void m1_prep_kernel(const uint8_t* __restrict_
             break;
         }
     }
-    ro[e] = miss >= 0 ? (uint8_t)miss : rg[e];
+    const uint8_t nr = miss >= 0 ? (uint8_t)miss : rg[e];
+    if (compact) rows_out[g] = nr;
+    else ro[e] = nr;
     eidx[g] = (uint8_t)e;
 }
 
@@ -187,6 +193,25 @@ __global__ void replicate_kernel(const uint8_t* __restrict__ data, uint8_t* __re
         const long long g = i / ((long long)m * bb);
         const long long b = i % bb;
         parity[i] = data[g * bb + b];   // k = 1: the group holds one block
+    }
+}
+
+// k <= 1, recovered-blocks layout: a block tagged anything but row 0 is a parity copy of
+// data row 0 (cauchy_256.cpp:1508-1516), so it is that row's recovered block.
+__global__ void rec_k1_kernel(const uint8_t* __restrict__ blocks, const uint8_t* __restrict__ rows_in,
+                              uint8_t* __restrict__ rec, uint8_t* __restrict__ rec_rows,
+                              int32_t* __restrict__ status, int bb, int rmax, long long groups) {
+    const long long total = groups * (long long)bb;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long g = i / bb;
+        const long long b = i % bb;
+        const bool lost = rows_in[g] != 0;
+        if (lost) rec[g * rmax * (long long)bb + b] = blocks[g * (long long)bb + b];
+        if (b == 0) {
+            rec_rows[g * rmax] = lost ? 0 : 255;
+            if (status) status[g] = 0;
+        }
     }
 }
 
@@ -371,7 +396,8 @@ __device__ __forceinline__ void prep_group(
     long long g, int lane, const uint8_t* gexp, const uint8_t* glog, const PrepScratch& sc,
     const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
     const uint8_t* cenc, uint8_t* __restrict__ coef, uint8_t* __restrict__ slots,
-    int32_t* __restrict__ nout, int k, int m, int bb, int rc, int rmax, int nchunk) {
+    int32_t* __restrict__ nout, uint8_t* __restrict__ rec_rows, int k, int m, int bb, int rc,
+    int rmax, int nchunk) {
     uint8_t* rowl = sc.rowl;
     uint8_t* present = sc.present;
     uint8_t* recpos = sc.recpos;
@@ -384,7 +410,8 @@ __device__ __forceinline__ void prep_group(
         recidx[i] = 255;
     }
     const uint8_t* rg = rows_in + g * k;
-    uint8_t* ro = rows_out + g * k;
+    uint8_t* ro = rows_out ? rows_out + g * k : nullptr;   // null: recovered-blocks layout
+    uint8_t* rec = rec_rows ? rec_rows + g * rmax : nullptr;
     for (int i = lane; i < k; i += 64) rowl[i] = rg[i];
     wave_sync();
     for (int i = lane; i < k; i += 64)
@@ -416,8 +443,10 @@ __device__ __forceinline__ void prep_group(
     wave_sync();
 
     auto finish_unchanged = [&](int st) {
-        if (ro != rg)
+        if (ro && ro != rg)
             for (int i = lane; i < k; i += 64) ro[i] = rowl[i];
+        if (rec)
+            for (int j = lane; j < rmax; j += 64) rec[j] = 255;
         if (lane == 0) {
             nout[g] = 0;
             if (status) status[g] = st;
@@ -493,13 +522,15 @@ __device__ __forceinline__ void prep_group(
             coef[g * (long long)nchunk * k * rcp + ((long long)ch * k + pos) * rcp + jj] = cval;
         }
     }
-    if (ro != rg)
+    if (ro && ro != rg)
         for (int i = lane; i < k; i += 64) ro[i] = rowl[i];
     wave_sync();
     for (int j = lane; j < n; j += 64) {
         slots[g * rmax + j] = recpos[j];
-        ro[recpos[j]] = era[j];                                            // :791
+        if (ro) ro[recpos[j]] = era[j];                                    // :791
     }
+    if (rec)
+        for (int j = lane; j < rmax; j += 64) rec[j] = j < n ? era[j] : 255;
     if (lane == 0) {
         nout[g] = n;
         if (status) status[g] = 0;
@@ -509,8 +540,8 @@ __device__ __forceinline__ void prep_group(
 __global__ __launch_bounds__(256) void decode_prep_kernel(
     const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
     const uint8_t* __restrict__ cenc, uint8_t* __restrict__ coef, uint8_t* __restrict__ slots,
-    int32_t* __restrict__ nout, long long groups, int k, int m, int bb, int rc, int rmax,
-    int nchunk, int scratch_bytes) {
+    int32_t* __restrict__ nout, uint8_t* __restrict__ rec_rows, long long groups, int k, int m,
+    int bb, int rc, int rmax, int nchunk, int scratch_bytes) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* gexp = smem;              // 512
     uint8_t* glog = gexp + 512;        // 256
@@ -527,7 +558,7 @@ __global__ __launch_bounds__(256) void decode_prep_kernel(
     for (long long g = (long long)blockIdx.x * nwv + w; g < groups;
          g += (long long)gridDim.x * nwv)
         prep_group(g, lane, gexp, glog, sc, rows_in, rows_out, status, lcenc, coef, slots, nout,
-                   k, m, bb, rc, rmax, nchunk);
+                   rec_rows, k, m, bb, rc, rmax, nchunk);
 }
 
 // In-place decode with more recovered blocks than one wave holds: the chunks write to a
@@ -602,14 +633,15 @@ static int xor_unit(const void* a, const void* b, long long s1, long long s2, in
 
 template <int VS, bool DECODE>
 static void xor_flat_launch(const uint8_t* in, uint8_t* out, const uint8_t* eidx, int k, int bb,
-                            long long G, long long igs, long long ogs, hipStream_t st) {
+                            long long G, long long igs, long long ogs, hipStream_t st,
+                            long long es) {
     const int nu = (bb + VS - 1) / VS;
     const unsigned total = (unsigned)(G * nu);
     const unsigned nb = (total + 255) / 256;
     switch (k) {
-        case 10: xor_flat_kernel<VS, 10, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs); break;
-        case 32: xor_flat_kernel<VS, 32, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs); break;
-        default: xor_flat_kernel<VS, 0, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs); break;
+        case 10: xor_flat_kernel<VS, 10, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs, es); break;
+        case 32: xor_flat_kernel<VS, 32, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs, es); break;
+        default: xor_flat_kernel<VS, 0, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs, es); break;
     }
 }
 
@@ -627,16 +659,18 @@ static int num_cus() {
 
 template <bool DECODE>
 static hipError_t xor_any(const uint8_t* in, uint8_t* out, const uint8_t* eidx, int k, int bb,
-                          long long G, long long igs, long long ogs, hipStream_t st) {
+                          long long G, long long igs, long long ogs, hipStream_t st,
+                          long long es = -1) {
+    if (es < 0) es = bb;
     if (G <= 0) return hipSuccess;
-    if (igs == (long long)k * bb && xor_dma_ok(in, out, k, bb, ogs))
+    if (es == bb && igs == (long long)k * bb && xor_dma_ok(in, out, k, bb, ogs))
         return launch_xor_dma(in, out, eidx, nullptr, nullptr, nullptr, k, bb, G, ogs, DECODE, st);
     const int vs = xor_unit(in, out, igs, ogs, bb);
     const long long units = G * ((bb + vs - 1) / vs);
     if (units > 0xffffffffLL) return hipErrorInvalidValue;
-    if (vs == 16) xor_flat_launch<16, DECODE>(in, out, eidx, k, bb, G, igs, ogs, st);
-    else if (vs == 4) xor_flat_launch<4, DECODE>(in, out, eidx, k, bb, G, igs, ogs, st);
-    else xor_bytes_kernel<DECODE><<<(unsigned)((units + 255) / 256), 256, 0, st>>>(in, out, eidx, k, bb, units, igs, ogs);
+    if (vs == 16) xor_flat_launch<16, DECODE>(in, out, eidx, k, bb, G, igs, ogs, st, es);
+    else if (vs == 4) xor_flat_launch<4, DECODE>(in, out, eidx, k, bb, G, igs, ogs, st, es);
+    else xor_bytes_kernel<DECODE><<<(unsigned)((units + 255) / 256), 256, 0, st>>>(in, out, eidx, k, bb, units, igs, ogs, es);
     return hipGetLastError();
 }
 
@@ -648,19 +682,20 @@ hipError_t launch_xor_encode(const uint8_t* data, uint8_t* parity, int k, int bb
 
 hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t* rows_in,
                              uint8_t* rows_out, int32_t* status, uint8_t* eidx, int k, int bb,
-                             long long groups, hipStream_t st) {
+                             long long groups, hipStream_t st, bool compact) {
     if (groups <= 0) return hipSuccess;
     const long long gb = (long long)k * bb;
-    if (k <= 64 && xor_dma_ok(blocks, out, k, bb, gb))
+    const long long ogs = compact ? bb : gb;
+    if (k <= 64 && xor_dma_ok(blocks, out, k, bb, ogs))
         // single launch: the DMA kernel also does the erased-slot / missing-row bookkeeping
-        return launch_xor_dma(blocks, out, nullptr, rows_in, rows_out, status, k, bb, groups, gb,
-                              true, st);
+        return launch_xor_dma(blocks, out, nullptr, rows_in, rows_out, status, k, bb, groups, ogs,
+                              true, st, compact);
     m1_prep_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(rows_in, rows_out, status,
-                                                                     eidx, k, groups);
+                                                                     eidx, k, groups,
+                                                                     compact ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return xor_any<true>(blocks, out, eidx, k, bb, groups, (long long)k * bb, (long long)k * bb,
-                         st);
+    return xor_any<true>(blocks, out, eidx, k, bb, groups, gb, ogs, st, compact ? 0 : bb);
 }
 
 hipError_t launch_replicate(const uint8_t* data, uint8_t* parity, int m, int bb,
@@ -669,6 +704,16 @@ hipError_t launch_replicate(const uint8_t* data, uint8_t* parity, int m, int bb,
     const long long total = groups * m * (long long)bb;
     const unsigned nb = (unsigned)std::min<long long>((total + 255) / 256, 65536);
     replicate_kernel<<<nb, 256, 0, st>>>(data, parity, m, bb, groups);
+    return hipGetLastError();
+}
+
+hipError_t launch_rec_k1(const uint8_t* blocks, const uint8_t* rows_in, uint8_t* rec,
+                        uint8_t* rec_rows, int32_t* status, int bb, int rmax, long long groups,
+                        hipStream_t st) {
+    if (groups <= 0) return hipSuccess;
+    const long long total = groups * (long long)bb;
+    const unsigned nb = (unsigned)std::min<long long>((total + 255) / 256, 65536);
+    rec_k1_kernel<<<nb, 256, 0, st>>>(blocks, rows_in, rec, rec_rows, status, bb, rmax, groups);
     return hipGetLastError();
 }
 
@@ -748,7 +793,7 @@ hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t*
 
 hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
                               const uint8_t* cenc, DecodeWork w, int k, int m, int bb, int rc,
-                              int rmax, long long groups, hipStream_t st) {
+                              int rmax, long long groups, hipStream_t st, uint8_t* rec_rows) {
     if (groups <= 0) return hipSuccess;
     const int nchunk = (rmax + rc - 1) / rc;
     const int scratch = (int)((1280 + (size_t)rmax * 2 * rmax + 15) & ~(size_t)15);
@@ -759,8 +804,8 @@ hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t
     const long long want = (groups + nwv - 1) / nwv;
     const unsigned nb = (unsigned)std::min<long long>(want, (long long)num_cus() * 16);
     decode_prep_kernel<<<nb, nwv * 64, lds, st>>>(rows_in, rows_out, status, cenc, w.coef,
-                                                   w.slots, w.nout, groups, k, m, bb, rc, rmax,
-                                                   nchunk, scratch);
+                                                   w.slots, w.nout, rec_rows, groups, k, m, bb,
+                                                   rc, rmax, nchunk, scratch);
     return hipGetLastError();
 }
 

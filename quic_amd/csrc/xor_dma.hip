@@ -34,10 +34,11 @@ __device__ __forceinline__ void xor_wait_vmcnt() {
 
 // m = 1 decode bookkeeping for one group, done by the wave that decodes it (k <= 64, one
 // row tag per lane; cauchy_decode_m1, cauchy_256.cpp:486-540).  `r` is this lane's row
-// tag (lanes >= k hold 255).  Returns the erased slot (-1 if none) and writes rows_out /
-// status.
+// tag (lanes >= k hold 255).  Returns the erased slot (-1 if none) and writes status and
+// either the rewritten row tags (ro, slot layout) or the recovered data row (rec,
+// recovered-blocks layout; 255 when nothing was erased).
 __device__ __forceinline__ int m1_rows_wave(int r, int k, uint8_t* flags, uint8_t* ro,
-                                            int32_t* status, long long g) {
+                                            uint8_t* rec, int32_t* status, long long g) {
     const int lane = threadIdx.x & 63;
     const unsigned long long er = __ballot(lane < k && r >= k);
     const int e = er ? __ffsll((long long)er) - 1 : -1;
@@ -49,21 +50,29 @@ __device__ __forceinline__ int m1_rows_wave(int r, int k, uint8_t* flags, uint8_
     if (lane < k) {
         int v = r;
         if (lane == e && miss) v = __ffsll((long long)miss) - 1;
-        ro[lane] = (uint8_t)v;
+        if (ro) ro[lane] = (uint8_t)v;
+        if (rec && lane == e) rec[0] = (uint8_t)v;
     }
+    if (rec && e < 0 && lane == 0) rec[0] = 255;
     if (status && lane == 0) status[g] = 0;
     return e;
 }
 
 // FUSED (decode only): rows_in/rows_out are handled here; otherwise eidx[g] names the
 // erased slot (255 = none), prepared by m1_prep_kernel.
-template <int NDMA, int NSLOT, bool DECODE, bool FUSED>
+// PROBE (tools/microbench/xor_dec_mb.hip only; the library instantiates 0), decode
+// timing probes: bit 0 = skip the row bookkeeping (slot 0 is taken as the erased one),
+// bit 1 = write the result densely at out + g * bb, bit 2 = no tag DMA, bit 3 = plain
+// (write-back) stores for the encode too.
+// COMPACT (decode): recovered-blocks layout, the result of group g goes to out + g * bb and
+// its data row to rows_out[g] (see qfec_decode_batch_recovered).
+template <int NDMA, int NSLOT, bool DECODE, bool FUSED, int PROBE = 0, bool COMPACT = false>
 __global__ __launch_bounds__(256) void xor_dma_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ eidx,
     const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
     int k, int bb, long long groups, long long out_gstride) {
     constexpr int SLOT = NDMA * 1024;
-    constexpr int R = DECODE ? 1 : 0;                 // row-tag loads per group
+    constexpr int R = (DECODE && !(PROBE & 4)) ? 1 : 0;   // row-tag loads per group
     constexpr int WAIT = (NSLOT - 1) * (NDMA + R);
     constexpr int kTagBytes = 80;                     // 16-byte multiple >= 64 + 6
     static_assert(WAIT <= 63, "too many DMA instructions in flight for vmcnt");
@@ -97,7 +106,7 @@ __global__ __launch_bounds__(256) void xor_dma_kernel(
             __builtin_amdgcn_global_load_lds(QX_GPTR(src + off),
                                              QX_LPTR(myl + slot * SLOT + p * 1024), 16, 0, 2);
         }
-        if (DECODE) {
+        if (DECODE && !(PROBE & 4)) {
             const uintptr_t t = tag_addr(gg);
             const uintptr_t t0 = t & ~(uintptr_t)3;
             const int nd = (int)((t + (fused ? k : 1) + 3 - t0) >> 2);   // dwords, <= 18
@@ -126,11 +135,14 @@ __global__ __launch_bounds__(256) void xor_dma_kernel(
             }
             const long long g = g0 + i * W;
             int e = 0;
-            if (DECODE) {
+            if (DECODE && (PROBE & 1)) {
+                e = 0;
+            } else if (DECODE) {
                 const uint8_t* tg = tagl + u * kTagBytes + (tag_addr(g) & 3);
                 if (fused) {
                     const int r = lane < k ? tg[lane] : 255;
-                    e = m1_rows_wave(r, k, flags, rows_out + g * k, status, g);
+                    e = COMPACT ? m1_rows_wave(r, k, flags, nullptr, rows_out + g, status, g)
+                                : m1_rows_wave(r, k, flags, rows_out + g * k, nullptr, status, g);
                 } else {
                     e = tg[0];
                     if (e == 255) e = -1;
@@ -138,7 +150,8 @@ __global__ __launch_bounds__(256) void xor_dma_kernel(
             }
             if (!DECODE || e >= 0) {
                 const uint8_t* L = myl + u * SLOT;
-                uint8_t* o = out + g * out_gstride + (long long)e * bb;
+                uint8_t* o = (COMPACT || (PROBE & 2)) ? out + g * (long long)bb
+                                                      : out + g * out_gstride + (long long)e * bb;
                 for (int q = lane; q < nq; q += 64) {
                     uint64_t acc = *(const uint64_t*)(L + q * 8);
                     int x = 1;
@@ -146,7 +159,12 @@ __global__ __launch_bounds__(256) void xor_dma_kernel(
                         acc ^= *(const uint64_t*)(L + x * bb + q * 8) ^
                                *(const uint64_t*)(L + (x + 1) * bb + q * 8);
                     if (x < k) acc ^= *(const uint64_t*)(L + x * bb + q * 8);
-                    __builtin_nontemporal_store(acc, (uint64_t*)(o + q * 8));
+                    // Decode writes one block per group, 13.5 KB apart in [G][k][bb]: plain
+                    // write-back stores measured 3 % faster there than nt (6 % in place,
+                    // where the slot's lines were just read); encode's dense parity
+                    // stream is faster with nt (tools/microbench/xor_dec_mb.hip).
+                    if ((DECODE && !COMPACT) || (PROBE & 8)) *(uint64_t*)(o + q * 8) = acc;
+                    else __builtin_nontemporal_store(acc, (uint64_t*)(o + q * 8));
                 }
             }
         }
@@ -193,7 +211,7 @@ bool xor_plan(int k, int bb, XorPlan* p) {
     return p->ndma <= 20;
 }
 
-template <bool DECODE, bool FUSED, int NSLOT, int N>
+template <bool DECODE, bool FUSED, bool COMPACT, int NSLOT, int N>
 hipError_t xor_go(const XorPlan& p, const uint8_t* in, uint8_t* out, const uint8_t* eidx,
                   const uint8_t* rows_in, uint8_t* rows_out, int32_t* status, int k, int bb,
                   long long G, long long ogs, hipStream_t st) {
@@ -201,24 +219,24 @@ hipError_t xor_go(const XorPlan& p, const uint8_t* in, uint8_t* out, const uint8
         return hipErrorInvalidValue;
     } else {
         if (p.ndma != N)
-            return xor_go<DECODE, FUSED, NSLOT, N + 1>(p, in, out, eidx, rows_in, rows_out, status, k,
+            return xor_go<DECODE, FUSED, COMPACT, NSLOT, N + 1>(p, in, out, eidx, rows_in, rows_out, status, k,
                                                 bb, G, ogs, st);
         const long long want = (G + p.waves - 1) / p.waves;
         const unsigned nb = (unsigned)std::min<long long>(want, (long long)xor_cus());
-        xor_dma_kernel<N, NSLOT, DECODE, FUSED><<<nb, p.waves * 64, p.lds, st>>>(
+        xor_dma_kernel<N, NSLOT, DECODE, FUSED, 0, COMPACT><<<nb, p.waves * 64, p.lds, st>>>(
             in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs);
         return hipGetLastError();
     }
 }
 
-template <bool DECODE, bool FUSED>
+template <bool DECODE, bool FUSED, bool COMPACT = false>
 hipError_t xor_dispatch(const XorPlan& p, const uint8_t* in, uint8_t* out, const uint8_t* eidx,
                         const uint8_t* rows_in, uint8_t* rows_out, int32_t* status, int k,
                         int bb, long long G, long long ogs, hipStream_t st) {
     switch (p.nslot) {
-        case 2: return xor_go<DECODE, FUSED, 2, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st);
-        case 3: return xor_go<DECODE, FUSED, 3, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st);
-        case 4: return xor_go<DECODE, FUSED, 4, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st);
+        case 2: return xor_go<DECODE, FUSED, COMPACT, 2, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st);
+        case 3: return xor_go<DECODE, FUSED, COMPACT, 3, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st);
+        case 4: return xor_go<DECODE, FUSED, COMPACT, 4, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st);
         default: return hipErrorInvalidValue;
     }
 }
@@ -235,13 +253,16 @@ bool xor_dma_ok(const void* in, const void* out, int k, int bb, long long ogs) {
 hipError_t launch_xor_dma(const uint8_t* in, uint8_t* out, const uint8_t* eidx,
                           const uint8_t* rows_in, uint8_t* rows_out, int32_t* status, int k,
                           int bb, long long groups, long long out_gstride, bool decode,
-                          hipStream_t st) {
+                          hipStream_t st, bool compact) {
     if (groups <= 0) return hipSuccess;
     XorPlan p;
     if (!xor_plan(k, bb, &p)) return hipErrorInvalidValue;
     if (!decode)
         return xor_dispatch<false, false>(p, in, out, eidx, rows_in, rows_out, status, k, bb,
                                           groups, out_gstride, st);
+    if (rows_in && compact)
+        return xor_dispatch<true, true, true>(p, in, out, eidx, rows_in, rows_out, status, k,
+                                              bb, groups, out_gstride, st);
     if (rows_in)
         return xor_dispatch<true, true>(p, in, out, eidx, rows_in, rows_out, status, k, bb,
                                         groups, out_gstride, st);

@@ -148,6 +148,19 @@ class FecEngine:
             raise FecError(rc, "qfec_decode_batch")
         return rc
 
+    def decode_recovered(self, k, m, block_bytes, blocks, rows_in, rec, rec_rows, status=None,
+                         stream=None):
+        """Recovered-blocks layout: rec [G][min(k,m)][bb], rec_rows [G][min(k,m)] uint8
+        (data row of each recovered block, ascending; 255 = unused).  blocks / rows_in are
+        not modified."""
+        G = blocks.shape[0]
+        rc = self.lib.qfec_decode_batch_recovered(self._h, k, m, block_bytes, G, _dptr(blocks),
+                                                  _dptr(rows_in), _dptr(rec), _dptr(rec_rows),
+                                                  _dptr(status), _stream(stream, blocks))
+        if rc:
+            raise FecError(rc, "qfec_decode_batch_recovered")
+        return rc
+
     # host-pointer batch calls (synchronous; include H2D/D2H)
     def encode_host(self, k, m, block_bytes, data):
         data = np.ascontiguousarray(data, dtype=np.uint8)
@@ -199,6 +212,17 @@ def decode_host_into(engine, k, m, block_bytes, blocks_h, rows_h, status_h=None)
                                            None if status_h is None else _hptr(status_h))
     if rc:
         raise FecError(rc, "qfec_decode_batch_host")
+    return rc
+
+
+def decode_recovered_host_into(engine, k, m, block_bytes, blocks_h, rows_h, rec_h, rec_rows_h,
+                               status_h=None):
+    """Host-pointer decode returning only the recovered blocks (CPU tensors)."""
+    rc = engine.lib.qfec_decode_batch_recovered_host(
+        engine._h, k, m, block_bytes, blocks_h.shape[0], _hptr(blocks_h), _hptr(rows_h),
+        _hptr(rec_h), _hptr(rec_rows_h), None if status_h is None else _hptr(status_h))
+    if rc:
+        raise FecError(rc, "qfec_decode_batch_recovered_host")
     return rc
 
 

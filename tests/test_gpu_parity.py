@@ -225,3 +225,113 @@ def test_full_size_round_trip(engine, oracle, k, m, bb, r):
     d_np = host(data[sample])
     p_or, _ = oracle.encode_batch(k, m, bb, d_np)
     np.testing.assert_array_equal(host(parity[sample]), p_or)
+
+
+# ------------------------------------------------- recovered-blocks layout (receiver)
+def expected_recovered(k, m, bb, rows_in, b_or, r_or, s_or):
+    """Recovered blocks in the order cauchy_256_decode assigns erased rows: the i-th
+    recovery slot (array order, row >= k) gets the i-th smallest erased row
+    (cauchy_256.cpp:570-574); m = 1 uses only the first such slot (:486-540)."""
+    G = rows_in.shape[0]
+    rmax = min(k, m)
+    rec = np.zeros((G, rmax, bb), np.uint8)
+    rec_rows = np.full((G, rmax), 255, np.uint8)
+    for g in range(G):
+        if s_or[g] != 0:
+            continue
+        if k <= 1:
+            if rows_in[g][0] != 0:
+                rec_rows[g][0] = 0
+                rec[g][0] = b_or[g][0]
+            continue
+        slots = [i for i in range(k) if rows_in[g][i] >= k]
+        if m == 1:
+            slots = slots[:1]
+        j = 0
+        for sl in slots:
+            if r_or[g][sl] < k and r_or[g][sl] != rows_in[g][sl]:
+                rec_rows[g][j] = r_or[g][sl]
+                rec[g][j] = b_or[g][sl]
+                j += 1
+    return rec, rec_rows
+
+
+@pytest.mark.parametrize("k,m,bb,r,shuffle", [
+    (10, 1, 1352, 1, False), (10, 1, 1352, 0, False), (10, 1, 1350, 1, True),
+    (32, 4, 1352, 2, True), (32, 4, 1352, 4, False), (8, 4, 64, 3, True),
+    (16, 8, 9008, 8, False), (128, 16, 1352, 11, True), (4, 4, 64, 0, False),
+    (20, 10, 64, 10, True),
+])
+def test_decode_recovered_vs_oracle(engine, oracle, k, m, bb, r, shuffle):
+    import torch
+    G = 6
+    data = synth.group_data(4321 + k + m, k, bb, G)
+    p_or, _ = oracle.encode_batch(k, m, bb, data)
+    rows, src = synth.loss_patterns(k, m, r, G, 55 + bb, shuffle=shuffle)
+    recv = synth.assemble_received(data, p_or, src)
+    b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+    exp, exp_rows = expected_recovered(k, m, bb, rows, b_or, r_or, s_or)
+    rmax = min(k, m)
+    b = dev(recv)
+    rw = dev(rows)
+    rec = torch.zeros((G, rmax, bb), dtype=torch.uint8, device="cuda")
+    rec_rows = torch.zeros((G, rmax), dtype=torch.uint8, device="cuda")
+    st = torch.full((G,), 7, dtype=torch.int32, device="cuda")
+    engine.decode_recovered(k, m, bb, b, rw, rec, rec_rows, status=st)
+    np.testing.assert_array_equal(host(st), s_or)
+    got_rows = host(rec_rows)
+    np.testing.assert_array_equal(got_rows, exp_rows)
+    got = host(rec)
+    mask = exp_rows != 255
+    np.testing.assert_array_equal(got[mask], exp[mask])
+    # recovered blocks are the original data rows
+    for g in range(G):
+        for j in range(rmax):
+            if got_rows[g][j] != 255:
+                np.testing.assert_array_equal(got[g][j], data[g][got_rows[g][j]])
+    # inputs untouched
+    np.testing.assert_array_equal(host(b), recv)
+    np.testing.assert_array_equal(host(rw), rows)
+
+
+def test_decode_recovered_k1_and_unsupported(engine, oracle):
+    import torch
+    # k = 1: a parity block is a copy of data row 0
+    k, m, bb, G = 1, 3, 64, 4
+    data = synth.group_data(9, k, bb, G)
+    rows = np.array([[0], [1], [3], [2]], np.uint8)
+    rec = torch.zeros((G, 1, bb), dtype=torch.uint8, device="cuda")
+    rr = torch.zeros((G, 1), dtype=torch.uint8, device="cuda")
+    engine.decode_recovered(k, m, bb, dev(data), dev(rows), rec, rr)
+    assert host(rr)[:, 0].tolist() == [255, 0, 0, 0]
+    np.testing.assert_array_equal(host(rec)[1:, 0], data[1:, 0])
+    # k + m > 256: status -1, nothing recovered
+    k, m, bb, G = 250, 7, 16, 2
+    data = synth.group_data(5, k, bb, G)
+    rows = np.tile(np.array(list(range(1, 250)) + [250], np.uint8), (G, 1))
+    rec = torch.zeros((G, 7, bb), dtype=torch.uint8, device="cuda")
+    rr = torch.zeros((G, 7), dtype=torch.uint8, device="cuda")
+    st = torch.zeros((G,), dtype=torch.int32, device="cuda")
+    engine.decode_recovered(k, m, bb, dev(data), dev(rows), rec, rr, status=st)
+    assert host(st).tolist() == [-1, -1]
+    assert (host(rr) == 255).all()
+
+
+def test_decode_recovered_host(engine, oracle):
+    import torch
+    k, m, bb, G, r = 32, 4, 1352, 40, 3
+    data = synth.group_data(77, k, bb, G)
+    p_or, _ = oracle.encode_batch(k, m, bb, data)
+    rows, src = synth.loss_patterns(k, m, r, G, 8, shuffle=True)
+    recv = synth.assemble_received(data, p_or, src)
+    b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+    exp, exp_rows = expected_recovered(k, m, bb, rows, b_or, r_or, s_or)
+    rec = torch.zeros((G, 4, bb), dtype=torch.uint8)
+    rr = torch.zeros((G, 4), dtype=torch.uint8)
+    st = torch.zeros((G,), dtype=torch.int32)
+    fec.decode_recovered_host_into(engine, k, m, bb, torch.from_numpy(recv),
+                                   torch.from_numpy(rows), rec, rr, st)
+    np.testing.assert_array_equal(rr.numpy(), exp_rows)
+    mask = exp_rows != 255
+    np.testing.assert_array_equal(rec.numpy()[mask], exp[mask])
+    assert st.abs().max() == 0
