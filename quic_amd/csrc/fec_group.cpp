@@ -200,13 +200,15 @@ class QuicFecGroup {
         return true;
     }
 
-    // Extraction after the decode (:280-293).
+    // Extraction after the decode (:280-293).  `blocks` / `rows` hold `nblk` decoded blocks
+    // and their row tags: all k of the in-place layout, or the recovered ones only.
     void SetRevived(const std::vector<uint64_t>& missing, const unsigned char* blocks,
-                    const unsigned char* rows, int bb, int status) {
+                    const unsigned char* rows, int bb, int status, size_t nblk = 0) {
+        if (nblk == 0) nblk = k_;
         rev_.clear();
         for (uint64_t pn : missing) {
             const unsigned char* payload = nullptr;
-            for (size_t i = 0; i < k_; ++i)
+            for (size_t i = 0; i < nblk; ++i)
                 if (rows[i] == (unsigned char)(pn - min_)) {
                     payload = blocks + i * bb;
                     break;
@@ -318,18 +320,24 @@ int flush_dec(qfec_batch* b, const std::tuple<int, int, int>& key) {
     if (v.empty()) return 0;
     const int k = std::get<0>(key), m = std::get<1>(key), bb = std::get<2>(key);
     const size_t G = v.size();
-    b->hbuf.resize(G * (size_t)k * bb);
-    b->hrows.resize(G * (size_t)k);
+    const size_t rmax = (size_t)std::min(k, m);
+    // inputs [G][k][bb] + [G][k]; outputs: only the recovered blocks (rmax per group)
+    b->hbuf.resize(G * ((size_t)k + rmax) * bb);
+    b->hrows.resize(G * ((size_t)k + rmax));
     b->hstatus.assign(G, 0);
+    unsigned char* in = b->hbuf.data();
+    unsigned char* rec = in + G * (size_t)k * bb;
+    unsigned char* rows = b->hrows.data();
+    unsigned char* rec_rows = rows + G * (size_t)k;
     for (size_t i = 0; i < G; ++i) {
-        memcpy(b->hbuf.data() + i * (size_t)k * bb, v[i].blocks.data(), (size_t)k * bb);
-        memcpy(b->hrows.data() + i * (size_t)k, v[i].rows.data(), (size_t)k);
+        memcpy(in + i * (size_t)k * bb, v[i].blocks.data(), (size_t)k * bb);
+        memcpy(rows + i * (size_t)k, v[i].rows.data(), (size_t)k);
     }
-    const int rc = qfec_decode_batch_host(b->ctx, k, m, bb, (long long)G, b->hbuf.data(),
-                                          b->hrows.data(), b->hstatus.data());
+    const int rc = qfec_decode_batch_recovered_host(b->ctx, k, m, bb, (long long)G, in, rows,
+                                                    rec, rec_rows, b->hstatus.data());
     for (size_t i = 0; i < G; ++i)
-        v[i].g->g.SetRevived(v[i].missing, b->hbuf.data() + i * (size_t)k * bb,
-                             b->hrows.data() + i * (size_t)k, bb, rc ? rc : b->hstatus[i]);
+        v[i].g->g.SetRevived(v[i].missing, rec + i * rmax * bb, rec_rows + i * rmax, bb,
+                             rc ? rc : b->hstatus[i], rmax);
     v.clear();
     return rc ? rc : (int)G;
 }
