@@ -203,13 +203,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # QFEC_BENCH_BACKEND=gloo rehearses the N>1 control flow with several ranks sharing
+    # one GPU (RCCL refuses two ranks on one device); the data path has no collective
+    # either way, only the barrier and the max-over-ranks of the elapsed time use it.
+    backend = os.environ.get("QFEC_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if world > 1 and backend == "gloo" and ndev > 0:
+        local = local % ndev
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from quic_amd import fec, shard, synth
     k, m, payload, r, label = WORKLOADS[args.workload]
@@ -277,7 +285,7 @@ def main():
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
 
-    elapsed = shard.max_over_ranks(elapsed, dev)
+    elapsed = shard.max_over_ranks(elapsed, dev if backend == "nccl" else None)
 
     ms_per_step = elapsed * 1e3 / args.steps
     total_groups = G * world
