@@ -14,10 +14,10 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
             -mllvm -structurizecfg-skip-uniform-regions=true \
             -DQFEC_BUILD -DQFEC_TABLES_PATH='"$(TABLES)"' -Wall -Wno-unused-function
 
-SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_group.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp
+SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_group.hip $(CSRC)/gf_stream.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp
 HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(CSRC)/gf_bitslice.h $(ROOT)include/quic_fec.h \
         $(ROOT)include/quic_fec_group.h $(ROOT)Makefile
-OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/xor_dma.o $(ROOT)build/gf_group.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o
+OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/xor_dma.o $(ROOT)build/gf_group.o $(ROOT)build/gf_stream.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o
 
 TOOL := $(ROOT)quic_amd/bin/fec_loopback
 
@@ -42,6 +42,10 @@ $(ROOT)build/xor_dma.o: $(CSRC)/xor_dma.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(ROOT)build/gf_group.o: $(CSRC)/gf_group.hip $(HDRS)
+	@mkdir -p $(ROOT)build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(ROOT)build/gf_stream.o: $(CSRC)/gf_stream.hip $(HDRS)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

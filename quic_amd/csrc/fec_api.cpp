@@ -238,6 +238,11 @@ int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     const uint8_t* tab = nullptr;
     int rcode = get_enc_table(c, k, m, rc, &tab);
     if (rcode) return rcode;
+    if (m <= rc && qfec::gf_stream_supported(k, m, bb, rc, false) && ((uintptr_t)d_data & 15) == 0) {
+        QF_HIP(qfec::launch_gf_stream(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc, 0, 0,
+                                      (long long)m * bb, false, st));
+        return 0;
+    }
     if (qfec::gf_group_supported(k, m, bb, rc)) {
         QF_HIP(qfec::launch_gf_group(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc,
                                      (m + rc - 1) / rc, 0, 0, (long long)m * bb, false, st));
@@ -272,6 +277,15 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc, rmax,
                                     G, st));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
+    if (nchunk == 1 && qfec::gf_stream_supported(k, m, bb, rc, true) &&
+        ((uintptr_t)d_blocks & 15) == 0) {
+        // a group's stores follow all of its reads: in place needs no scratch
+        const int rcp = std::max(rc, 4);
+        QF_HIP(qfec::launch_gf_stream(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
+                                      rmax, (long long)nchunk * k * rcp, (long long)k * bb, true,
+                                      st));
+        return 0;
+    }
     if (qfec::gf_group_supported(k, m, bb, rc)) {
         // whole group in LDS before any store: in place needs no scratch
         const int rcp = std::max(rc, 4);
@@ -324,6 +338,13 @@ int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
     QF_HIP(qfec::launch_decode_prep(d_rows_in, nullptr, d_status, cenc, w, k, m, bb, rc, rmax, G,
                                     st, d_rec_rows));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
+    if (rmax <= rc && qfec::gf_stream_supported(k, m, bb, rc, true) &&
+        ((uintptr_t)d_blocks & 15) == 0) {
+        const int rcp = std::max(rc, 4);
+        QF_HIP(qfec::launch_gf_stream(d_blocks, d_rec, w.coef, nullptr, w.nout, k, m, bb, G, rc,
+                                      rmax, (long long)k * rcp, (long long)rmax * bb, true, st));
+        return 0;
+    }
     QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, d_rec, w, k, m, bb, G, rc, rmax, st));
     return 0;
 }

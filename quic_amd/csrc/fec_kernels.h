@@ -79,6 +79,13 @@ hipError_t launch_xor_dma(const uint8_t* in, uint8_t* out, const uint8_t* eidx,
                           int bb, long long groups, long long out_gstride, bool decode,
                           hipStream_t st, bool compact = false);
 
+// Per-wave LDS-ring streaming kernel for bb = 1352, one output chunk (gf_stream.hip).
+bool gf_stream_supported(int k, int m, int bb, int rc, bool decode);
+hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef,
+                            const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
+                            long long groups, int rc, int rmax, long long coef_gstride,
+                            long long out_gstride, bool decode, hipStream_t st);
+
 // Whole-group LDS kernel for groups that fit in LDS (gf_group.hip).
 bool gf_group_supported(int k, int m, int bb, int rc);
 hipError_t launch_gf_group(const uint8_t* in, uint8_t* out, const uint8_t* coef,

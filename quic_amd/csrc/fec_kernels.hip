@@ -276,12 +276,17 @@ template <int RC> struct ApplyBound { static constexpr int T = RC <= 4 ? 1024 : 
 //   coef:  [(g) * coef_gstride + (chunk * k + pos) * RCP + j]  (RCP = max(4, RC))
 //   encode: outputs o = chunk*RC + j < m go to out + g*out_gstride + o*bb
 //   decode: outputs o < nout[g] go to out + g*out_gstride + slots[g*rmax + o]*bb
-template <int RC, bool DECODE, bool TINY, int PD>
+//   FLAT (encode only: the coefficients are the same for every group): the lanes of a wave
+//   take consecutive (group, column word) pairs across group boundaries, so no lane idles
+//   when a sub-row is not a multiple of 64 words (169-byte sub-rows: 43 words, 67 % of a
+//   wave); waves are numbered (lane tile, chunk) with the chunk fastest.
+template <int RC, bool DECODE, bool TINY, int PD, bool FLAT = false>
 __global__ __launch_bounds__(ApplyBound<RC>::T) void gf_apply_kernel(
     const uint8_t* __restrict__ in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, int k, int m, int bb,
     int nw, int ntiles, int nchunk, int rmax, long long coef_gstride, long long out_gstride,
-    int total_units) {
+    int total_units, long long flat_lanes = 0) {
+    static_assert(!(FLAT && DECODE), "decode coefficients differ per group");
     constexpr int RCP = RC < 4 ? 4 : RC;
     constexpr int NCW = RCP / 4;
     const int lane = threadIdx.x & 63;
@@ -294,19 +299,30 @@ __global__ __launch_bounds__(ApplyBound<RC>::T) void gf_apply_kernel(
     const unsigned lwg = xcd * q8 + (xcd < r8 ? xcd : r8) + (b >> 3);
     const int unit = (int)lwg * 4 + wave_id();
     if (unit >= total_units) return;
-    const int tile = unit % ntiles;
-    const int gc = unit / ntiles;
-    const int chunk = gc % nchunk;
-    const int g = gc / nchunk;
+    int g, chunk, c;
+    bool live = true;
+    if (FLAT) {
+        chunk = unit % nchunk;
+        long long u = (long long)(unit / nchunk) * 64 + lane;
+        live = u < flat_lanes;
+        if (!live) u = flat_lanes - 1;
+        g = (int)(u / nw);
+        c = (int)(u - (long long)g * nw);
+    } else {
+        const int tile = unit % ntiles;
+        const int gc = unit / ntiles;
+        chunk = gc % nchunk;
+        g = gc / nchunk;
+        c = tile * 64 + lane;
+    }
     int n = DECODE ? nout[g] : m;
     n = min(n - chunk * RC, RC);
     if (n <= 0) return;
     const int s = bb >> 3;
-    const int c = tile * 64 + lane;
     const ColAccess ca = col_access<TINY>(c, nw, s);
 
     const uint8_t* gin = in + (long long)g * k * bb;
-    const uint32_t* cw = (const uint32_t*)(coef + (long long)g * coef_gstride +
+    const uint32_t* cw = (const uint32_t*)(coef + (FLAT ? 0 : (long long)g * coef_gstride) +
                                            (long long)chunk * k * RCP);
 
     uint32_t acc[RC][8];
@@ -355,6 +371,7 @@ __global__ __launch_bounds__(ApplyBound<RC>::T) void gf_apply_kernel(
         }
     }
 
+    if (!live) return;
 #pragma unroll
     for (int j = 0; j < RC; ++j) {
         if (j < n) {
@@ -736,6 +753,16 @@ static int pd_choice() {
     return pd;
 }
 
+// Lane-flat encode (QFEC_FLAT=0 turns it off for experiments).
+static bool flat_choice() {
+    static int f = -1;
+    if (f < 0) {
+        const char* e = getenv("QFEC_FLAT");
+        f = e ? (atoi(e) != 0) : 1;
+    }
+    return f != 0;
+}
+
 template <bool DECODE>
 static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8_t* coef,
                                     const uint8_t* slots, const int32_t* nout, int k, int m,
@@ -745,32 +772,30 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
     const int s = bb / 8;
     const int nw = (s + 3) / 4;
     const int ntiles = (nw + 63) / 64;
-    const long long units = groups * nchunk * ntiles;
+    const bool flat = !DECODE && s >= 4 && flat_choice() && (nw & 63) != 0;
+    const long long flat_lanes = groups * nw;
+    const long long units = flat ? nchunk * ((flat_lanes + 63) / 64) : groups * nchunk * ntiles;
     if (units <= 0) return hipSuccess;
     if (units > 0x7fffffffLL) return hipErrorInvalidValue;
-    const int per_group = nchunk * ntiles;
     const unsigned nb = blocks_for_waves(units);
     const unsigned nthr = 256;
-    (void)per_group;
     const int tu = (int)units;
+    const int pd = pd_choice();
+#define QF_ARGS in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
+                out_gstride, tu, flat_lanes
 #define QF_LAUNCH(RCV)                                                                        \
     do {                                                                                      \
-        if (s >= 4 && pd_choice() == 3)                                                       \
-            gf_apply_kernel<RCV, DECODE, false, 3><<<nb, nthr, 0, st>>>(                      \
-                in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
-                out_gstride, tu);                                                             \
-        else if (s >= 4 && pd_choice() == 1)                                                  \
-            gf_apply_kernel<RCV, DECODE, false, 1><<<nb, nthr, 0, st>>>(                      \
-                in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
-                out_gstride, tu);                                                             \
+        if (flat) {                                                                           \
+            if constexpr (!DECODE)                                                            \
+                gf_apply_kernel<RCV, false, false, 2, true><<<nb, nthr, 0, st>>>(QF_ARGS);    \
+        } else if (s >= 4 && pd == 3)                                                         \
+            gf_apply_kernel<RCV, DECODE, false, 3><<<nb, nthr, 0, st>>>(QF_ARGS);             \
+        else if (s >= 4 && pd == 1)                                                           \
+            gf_apply_kernel<RCV, DECODE, false, 1><<<nb, nthr, 0, st>>>(QF_ARGS);             \
         else if (s >= 4)                                                                      \
-            gf_apply_kernel<RCV, DECODE, false, 2><<<nb, nthr, 0, st>>>(                      \
-                in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
-                out_gstride, tu);                                                             \
+            gf_apply_kernel<RCV, DECODE, false, 2><<<nb, nthr, 0, st>>>(QF_ARGS);             \
         else                                                                                  \
-            gf_apply_kernel<RCV, DECODE, true, 1><<<nb, nthr, 0, st>>>(                       \
-                in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
-                out_gstride, tu);                                                             \
+            gf_apply_kernel<RCV, DECODE, true, 1><<<nb, nthr, 0, st>>>(QF_ARGS);              \
     } while (0)
     switch (rc) {
         case 1: QF_LAUNCH(1); break;
@@ -781,6 +806,7 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
         default: return hipErrorInvalidValue;
     }
 #undef QF_LAUNCH
+#undef QF_ARGS
     return hipGetLastError();
 }
 

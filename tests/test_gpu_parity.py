@@ -335,3 +335,43 @@ def test_decode_recovered_host(engine, oracle):
     mask = exp_rows != 255
     np.testing.assert_array_equal(rec.numpy()[mask], exp[mask])
     assert st.abs().max() == 0
+
+
+# ------------------------------------------- gf_stream ring (many groups per wave)
+@pytest.mark.parametrize("ring", [4, 7, 10])
+@pytest.mark.parametrize("k,m,r", [(32, 4, 2), (32, 3, 3), (250, 5, 5), (32, 8, 6)])
+def test_stream_ring_many_groups_per_wave(engine, oracle, monkeypatch, ring, k, m, r):
+    """One workgroup (4 waves) walks every group, so each wave streams several groups
+    through its LDS ring back to back (the ring wraps inside blocks and across groups);
+    every third group has no loss (decode skips it but its pieces stay in the stream)."""
+    import torch
+    monkeypatch.setenv("QFEC_STREAM_GRID", "1")
+    monkeypatch.setenv("QFEC_STREAM_RING", str(ring))
+    monkeypatch.setenv("QFEC_STREAM_ENC", "1")
+    bb, G = 1352, 23
+    data = synth.group_data(900 + k + m + ring, k, bb, G)
+    p_or, rc_or = oracle.encode_batch(k, m, bb, data)
+    p_gpu, rc = gpu_encode(engine, k, m, bb, data)
+    assert rc == rc_or == 0
+    np.testing.assert_array_equal(p_gpu, p_or)
+    rows, src = synth.loss_patterns(k, m, r, G, 31 + ring, shuffle=True)
+    rows[::3] = np.arange(k, dtype=rows.dtype)
+    src[::3] = np.arange(k, dtype=src.dtype)
+    recv = synth.assemble_received(data, p_or, src)
+    b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+    for inplace in (True, False):
+        b, rr, s = gpu_decode(engine, k, m, bb, recv, rows, inplace=inplace)
+        np.testing.assert_array_equal(s, s_or)
+        np.testing.assert_array_equal(rr, r_or)
+        np.testing.assert_array_equal(b, b_or)
+    exp, exp_rows = expected_recovered(k, m, bb, rows, b_or, r_or, s_or)
+    rmax = min(k, m)
+    rec = torch.zeros((G, rmax, bb), dtype=torch.uint8, device="cuda")
+    rec_rows = torch.zeros((G, rmax), dtype=torch.uint8, device="cuda")
+    st = torch.full((G,), 7, dtype=torch.int32, device="cuda")
+    engine.decode_recovered(k, m, bb, dev(recv), dev(rows), rec, rec_rows, status=st)
+    np.testing.assert_array_equal(host(st), s_or)
+    np.testing.assert_array_equal(host(rec_rows), exp_rows)
+    got = host(rec)
+    mask = exp_rows != 255
+    np.testing.assert_array_equal(got[mask], exp[mask])

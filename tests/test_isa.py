@@ -1,0 +1,53 @@
+"""ISA guard for the counted-vmcnt kernels (CPU only: hipcc cross-compiles gfx950).
+
+gf_stream_kernel (quic_amd/csrc/gf_stream.hip) keeps its own count of the VMEM
+instructions it issued and waits with `s_waitcnt vmcnt(N)` for exactly the pieces a
+block needs.  That is only sound if the compiler emits no VMEM instruction outside the
+count (a global_load of a uniform byte, say) and inserts no vmcnt wait of its own (which
+would drain the ring).  This test compiles the file and checks both."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = "/opt/rocm/bin/hipcc"
+COUNTED = {"global_load_lds_dwordx4", "buffer_store_dword", "buffer_store_short",
+           "buffer_store_byte"}
+
+
+@pytest.fixture(scope="module")
+def stream_isa(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("isa") / "gf_stream.s"
+    src = os.path.join(ROOT, "quic_amd", "csrc", "gf_stream.hip")
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    "-mllvm", "-structurizecfg-skip-uniform-regions=true", "-DQFEC_BUILD",
+                    "--cuda-device-only", "-S", "-o", str(out), src],
+                   check=True, capture_output=True)
+    text = out.read_text()
+    bodies = {}
+    for m in re.finditer(r"^(_ZN4qfec16gf_stream_kernel\w+):", text, re.M):
+        end = text.index(".Lfunc_end", m.end())
+        bodies[m.group(1)] = text[m.end():end]
+    assert len(bodies) >= 6, "expected RC 2/4/8 x encode/decode instantiations"
+    return bodies
+
+
+def test_only_counted_vmem(stream_isa):
+    for name, body in stream_isa.items():
+        ops = re.findall(r"^\s+((?:global|buffer|flat|scratch)_\w+)", body, re.M)
+        extra = sorted(set(ops) - COUNTED)
+        assert not extra, f"{name}: VMEM outside the vmcnt bookkeeping: {extra}"
+        assert "global_load_lds_dwordx4" in ops
+
+
+def test_no_compiler_vmcnt_waits(stream_isa):
+    for name, body in stream_isa.items():
+        lines = body.split("\n")
+        for i, line in enumerate(lines):
+            if "s_waitcnt" in line and "vmcnt" in line:
+                assert lines[i - 1].strip() == ";;#ASMSTART", \
+                    f"{name}: compiler-inserted wait: {line.strip()}"

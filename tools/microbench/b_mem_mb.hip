@@ -157,6 +157,73 @@ __global__ __launch_bounds__(256) void lds_group(const uint8_t* __restrict__ in,
     store_out(out, g, lane, acc);
 }
 
+
+// (e) lane-flat unaligned dword loads: lanes take consecutive (group, word) pairs across
+// group boundaries (every lane busy), PD blocks ahead
+template <int PD>
+__global__ __launch_bounds__(256) void reg_flat(const uint8_t* __restrict__ in, uint8_t* out, long long G) {
+    const long long u0 = ((long long)blockIdx.x * 4 + wid()) * 64;
+    const int lane = threadIdx.x & 63;
+    long long u = u0 + lane;
+    if (u0 >= G * NW) return;
+    const bool live = u < G * NW;
+    if (!live) u = G * NW - 1;
+    const long long g = u / NW;
+    const int c = (int)(u - g * NW);
+    const int off = min(4 * c, S - 4);
+    const uint8_t* p = in + g * K * BB + off;
+    uint32_t acc[8] = {0}, raw[PD][8];
+#pragma unroll
+    for (int q = 0; q < PD; ++q)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) raw[q][t] = *(const u32ua*)(p + q * BB + t * S);
+#pragma unroll
+    for (int x = 0; x < K; ++x) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] ^= raw[x % PD][t];
+        if (x + PD < K)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) raw[x % PD][t] = *(const u32ua*)(p + (x + PD) * BB + t * S);
+    }
+    if (live && c < 42) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) *(u32ua*)(out + g * BB + r * S + 4 * c) = acc[r];
+    }
+}
+
+// (f) one group per wave, one ALIGNED dword per lane per sub-row; the next dword comes from
+// lane + 1 over DPP (wave_shl:1) and v_alignbyte realigns
+template <int PD>
+__global__ __launch_bounds__(256) void reg_dpp(const uint8_t* __restrict__ in, uint8_t* out, long long G) {
+    const long long g = (long long)blockIdx.x * 4 + wid();
+    if (g >= G) return;
+    const int lane = threadIdx.x & 63;
+    const int c = lane < 44 ? lane : 43;
+    const uint8_t* base = in + g * K * BB;   // 8-byte aligned
+    uint32_t acc[8] = {0}, raw[PD][8];
+    auto ld = [&](int x, int t) -> uint32_t {
+        const int o = x * BB + t * S;   // o & 3 == t & 3 (BB % 8 == 0)
+        return *(const uint32_t*)(base + (o & ~3) + 4 * c);
+    };
+#pragma unroll
+    for (int q = 0; q < PD; ++q)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) raw[q][t] = ld(q, t);
+#pragma unroll
+    for (int x = 0; x < K; ++x) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const uint32_t cur = raw[x % PD][t];
+            const uint32_t nxt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cur, 0x130, 0xf, 0xf, false);
+            acc[t] ^= (t & 3) ? __builtin_amdgcn_alignbyte(nxt, cur, t & 3) : cur;
+        }
+        if (x + PD < K)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) raw[x % PD][t] = ld(x + PD, t);
+    }
+    store_out(out, g, lane, acc);
+}
+
 template <class F>
 void timeit(const char* name, F launch, double bytes, int reps) {
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -185,6 +252,11 @@ int main() {
     const int reps = 10;
     timeit("a reg_unaligned PD2", [&] { hipLaunchKernelGGL(reg_unaligned<2>, dim3(nb4), dim3(256), 0, 0, in, out, G); }, bytes, reps);
     timeit("a reg_unaligned PD4", [&] { hipLaunchKernelGGL(reg_unaligned<4>, dim3(nb4), dim3(256), 0, 0, in, out, G); }, bytes, reps);
+    const unsigned nbf = (unsigned)((G * NW + 255) / 256);
+    timeit("e reg_flat PD2", [&] { hipLaunchKernelGGL(reg_flat<2>, dim3(nbf), dim3(256), 0, 0, in, out, G); }, bytes, reps);
+    timeit("e reg_flat PD4", [&] { hipLaunchKernelGGL(reg_flat<4>, dim3(nbf), dim3(256), 0, 0, in, out, G); }, bytes, reps);
+    timeit("f reg_dpp PD2", [&] { hipLaunchKernelGGL(reg_dpp<2>, dim3(nb4), dim3(256), 0, 0, in, out, G); }, bytes, reps);
+    timeit("f reg_dpp PD4", [&] { hipLaunchKernelGGL(reg_dpp<4>, dim3(nb4), dim3(256), 0, 0, in, out, G); }, bytes, reps);
     timeit("b reg_aligned PD2", [&] { hipLaunchKernelGGL(reg_aligned<2>, dim3(nb4), dim3(256), 0, 0, in, out, G); }, bytes, reps);
     timeit("b reg_aligned PD4", [&] { hipLaunchKernelGGL(reg_aligned<4>, dim3(nb4), dim3(256), 0, 0, in, out, G); }, bytes, reps);
     timeit("c lds_ring NS4", [&] { hipLaunchKernelGGL(lds_ring<4>, dim3(nb4), dim3(256), 4 * 4 * 1376, 0, in, out, G); }, bytes, reps);
