@@ -578,6 +578,232 @@ __global__ __launch_bounds__(256) void decode_prep_kernel(
                    rec_rows, k, m, bb, rc, rmax, nchunk);
 }
 
+// Decode prep with four LANES per group, for small erasure counts (rmax <= 4, k <= 64: the
+// 1350-byte configs).  Same bookkeeping, status codes and outputs as prep_group above
+// (cauchy_256.cpp:543-575, :791, :1287-1294); the r x r inverse and the per-slot
+// coefficients are computed in registers with the GF(256) log/exp tables in LDS, so a
+// group costs a few hundred independent LDS reads instead of a chain of wave-wide LDS
+// round trips (prep_group: ~90 us for 65,536 (32, 4) groups, most of it latency).
+// Packed small lists: byte j of recpos/recrow/era = entry j (j < 4).
+__global__ __launch_bounds__(256) void decode_prep_lane_kernel(
+    const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
+    const uint8_t* __restrict__ cenc, uint8_t* __restrict__ coef, uint8_t* __restrict__ slots,
+    int32_t* __restrict__ nout, uint8_t* __restrict__ rec_rows, long long groups, int k, int m,
+    int bb, int rmax) {
+    // LDS: exp/log tables, the m x k encode matrix, the block's row tags [256][k] (loaded
+    // coalesced) and its coefficient dwords [256][k + 1] (stored coalesced at the end)
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    extern __shared__ __attribute__((aligned(16))) uint8_t lsm[];
+    uint8_t* lcenc = lsm;                                       // m x k (padded to 16)
+    constexpr int LPG = 4;                                      // lanes per group
+    constexpr int GPB = 256 / LPG;                              // groups per block
+    uint8_t* lrows = lsm + ((m * k + 15) & ~15);                // GPB x k
+    uint32_t* lcoef = (uint32_t*)(lrows + GPB * k);             // GPB x (k + 1), k % 4 == 0
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) gexp[i] = c_gf.exp[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) glog[i] = c_gf.log[i];
+    for (int i = threadIdx.x; i < m * k; i += blockDim.x) lcenc[i] = cenc[i];
+    const long long gfirst = (long long)blockIdx.x * GPB;
+    const int ng = (int)min((long long)GPB, groups - gfirst);
+    {
+        const uint32_t* src = (const uint32_t*)(rows_in + gfirst * k);   // 4-byte aligned
+        const int nd = ng * k / 4;
+#pragma unroll 4
+        for (int i = threadIdx.x; i < nd; i += blockDim.x) ((uint32_t*)lrows)[i] = src[i];
+    }
+    __syncthreads();
+    // LPG lanes per group: each runs the bookkeeping and the r x r inverse (cheap) and
+    // computes the coefficients of every LPG-th input slot; lane q == 0 writes the rest
+    const int gl = threadIdx.x / LPG, q = threadIdx.x % LPG;
+    const long long g = gfirst + gl;
+    const bool live = gl < ng;
+    const bool lead = live && q == 0;
+    const uint8_t* rg = lrows + gl * k;                         // this group's tags (LDS)
+    const uint8_t* rgg = rows_in + g * k;
+    uint8_t* ro = rows_out ? rows_out + g * k : nullptr;
+    uint8_t* rec = rec_rows ? rec_rows + g * rmax : nullptr;
+    uint32_t* mycoef = lcoef + gl * (k + 1);
+    // every lane runs the body (dead lanes on a copy of lane 0's tags, no global writes)
+    // so that the block reaches the coalesced coefficient store together
+    if (!live) rg = lrows;
+
+    // tags four at a time (k % 4 == 0, rows 4-byte aligned in LDS)
+    const uint32_t* rg4 = (const uint32_t*)rg;
+    uint64_t present = 0;
+    int nrec = 0;
+    uint32_t recpos = 0, recrow = 0;
+    for (int i4 = 0; i4 < k; i4 += 4) {
+        const uint32_t t4 = rg4[i4 >> 2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i4 + u;
+            const int r = (int)((t4 >> (8 * u)) & 0xFF);
+            if (r < k) {
+                present |= 1ull << r;
+            } else {
+                if (nrec < 4) {
+                    recpos |= (uint32_t)i << (8 * nrec);
+                    recrow |= (uint32_t)(r - k < 255 ? r - k : 255) << (8 * nrec);
+                }
+                ++nrec;
+            }
+        }
+    }
+    const uint64_t kmask = k == 64 ? ~0ull : ((1ull << k) - 1);
+    uint64_t missing = ~present & kmask;
+    const int nera = __popcll(missing);
+
+    // a group left unchanged writes no coefficients (nout = 0: the apply skips it)
+    auto finish_unchanged = [&](int st) {
+        if (!lead) return;
+        if (ro && ro != rgg)
+            for (int i = 0; i < k; ++i) ro[i] = rg[i];
+        if (rec)
+            for (int j = 0; j < rmax; ++j) rec[j] = 255;
+        nout[g] = 0;
+        if (status) status[g] = st;
+    };
+    int early = 1;   // status of a group that needs no coefficients; 1 = go on
+    if (nrec == 0) early = 0;                                               // :1287-1289
+    else if (k + m > 256 || (bb & 7)) early = -1;                           // :1292-1294
+    else if (nrec > rmax || nera < nrec) early = -3;                        // malformed rows
+    else
+        for (int i = 0; i < nrec; ++i)
+            if ((int)((recrow >> (8 * i)) & 0xFF) >= m) early = -3;         // row >= k + m
+    const int n = early == 1 ? nrec : 0;
+    uint32_t era = 0;
+    for (int j = 0; j < n; ++j) {
+        const int e = __ffsll((long long)missing) - 1;
+        missing &= missing - 1;
+        era |= (uint32_t)e << (8 * j);
+    }
+    auto B = [](uint32_t v, int j) -> int { return (int)((v >> (8 * j)) & 0xFF); };
+    auto mul = [&](int a, int b) -> int { return (a && b) ? gexp[glog[a] + glog[b]] : 0; };
+
+    // [S | I], S[i][j] = C[y_i][e_j]; Gauss-Jordan fully unrolled over the 4 x 8 maximum
+    uint8_t M[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint8_t v = 0;
+            if (i < n && j < n) v = lcenc[B(recrow, i) * k + B(era, j)];
+            else if (i < n && j >= 4) v = (j - 4 == i) ? 1 : 0;
+            M[i][j] = v;
+        }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        if (p < n) {
+            int piv = -1;
+#pragma unroll
+            for (int i = 3; i >= p; --i)
+                if (i < n && M[i][p] != 0) piv = i;
+            if (piv < 0) {                                                  // singular
+                early = -3;
+                piv = p;
+            }
+#pragma unroll
+            for (int i = p + 1; i < 4; ++i) {
+                if (i == piv) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint8_t t = M[p][j];
+                        M[p][j] = M[i][j];
+                        M[i][j] = t;
+                    }
+                }
+            }
+            const int inv = M[p][p] ? gexp[255 - glog[M[p][p]]] : 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) M[p][j] = (uint8_t)mul(M[p][j], inv);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (i != p && i < n) {
+                    const int f = M[i][p];
+                    if (f) {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) M[i][j] ^= (uint8_t)mul(f, M[p][j]);
+                    }
+                }
+            }
+        }
+    }
+    // log of S^-1 (256 = zero)
+    int lsi[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int v = (j < n && i < n) ? M[j][4 + i] : 0;
+            lsi[j][i] = v ? glog[v] : 256;
+        }
+    // coefficient dword per input slot: byte j = recovered row j's coefficient
+    for (int pos4 = 4 * q; pos4 < k; pos4 += 4 * LPG) {
+      const uint32_t t4 = rg4[pos4 >> 2];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {   // four independent lookup chains
+        const int pos = pos4 + u;
+        int ri = -1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (i < n && B(recpos, i) == pos) ri = i;
+        uint32_t cw = 0;
+        if (ri >= 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (j < n) {
+                    int v = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (i == ri) v = M[j][4 + i];
+                    cw |= (uint32_t)v << (8 * j);
+                }
+        } else if (n > 0) {
+            const int x = (int)((t4 >> (8 * u)) & 0xFF);
+            int acc[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (i < n) {
+                    const int cv = lcenc[B(recrow, i) * k + x];
+                    if (cv) {
+                        const int lc = glog[cv];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (j < n && lsi[j][i] != 256) acc[j] ^= gexp[lsi[j][i] + lc];
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cw |= (uint32_t)acc[j] << (8 * j);
+        }
+        mycoef[pos] = cw;
+      }
+    }
+    if (early != 1) {
+        finish_unchanged(early);
+    } else if (lead) {
+        if (ro && ro != rgg)
+            for (int i = 0; i < k; ++i) ro[i] = rg[i];
+        for (int j = 0; j < n; ++j) {
+            slots[g * rmax + j] = (uint8_t)B(recpos, j);
+            if (ro) ro[B(recpos, j)] = (uint8_t)B(era, j);                // :791
+        }
+        if (rec)
+            for (int j = 0; j < rmax; ++j) rec[j] = j < n ? (uint8_t)B(era, j) : 255;
+        nout[g] = n;
+        if (status) status[g] = 0;
+    }
+    __syncthreads();
+    // coalesced store of the block's coefficient rows [ng][k] dwords
+    uint32_t* cdst = (uint32_t*)(coef + gfirst * (long long)k * 4);
+    const int nd = ng * k;
+#pragma unroll 4
+    for (int d = threadIdx.x; d < nd; d += blockDim.x) {
+        const int gg = d / k;
+        cdst[d] = lcoef[gg * (k + 1) + (d - gg * k)];
+    }
+}
+
 // In-place decode with more recovered blocks than one wave holds: the chunks write to a
 // [G][rmax][bb] scratch, then this copies each recovered block into its slot.
 __global__ __launch_bounds__(256) void scatter_recovered_kernel(
@@ -821,6 +1047,17 @@ hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t
                               const uint8_t* cenc, DecodeWork w, int k, int m, int bb, int rc,
                               int rmax, long long groups, hipStream_t st, uint8_t* rec_rows) {
     if (groups <= 0) return hipSuccess;
+    static const int lane_prep = getenv("QFEC_PREP_LANE") ? atoi(getenv("QFEC_PREP_LANE")) : 1;
+    if (lane_prep && rmax <= 4 && k <= 64 && k % 4 == 0 && (long long)m * k <= 4096 && rc <= 4 &&
+        ((((uintptr_t)w.coef) | (uintptr_t)rows_in) & 3) == 0) {
+        const unsigned nb = (unsigned)((groups + 63) / 64);     // 64 groups x 4 lanes
+        const size_t lds = (((size_t)m * k + 15) & ~(size_t)15) + 64 * (size_t)k +
+                           64 * (size_t)(k + 1) * 4;
+        decode_prep_lane_kernel<<<nb, 256, lds, st>>>(
+            rows_in, rows_out, status, cenc, w.coef, w.slots, w.nout, rec_rows, groups, k, m, bb,
+            rmax);
+        return hipGetLastError();
+    }
     const int nchunk = (rmax + rc - 1) / rc;
     const int scratch = (int)((1280 + (size_t)rmax * 2 * rmax + 15) & ~(size_t)15);
     const size_t fixed = 768 + (((size_t)m * k + 15) & ~(size_t)15);
