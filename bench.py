@@ -86,9 +86,26 @@ def cpu_baseline(k, m, bb, payload, r, data_h, blocks_h, rows_h, seconds):
 # Which template argument of each kernel says "decode" (bool): the PMC summaries are split
 # into the encode and the decode phase by it.
 _DECODE_ARG = {"xor_dma_kernel": 2, "gf_apply_kernel": 1, "gf_ring_kernel": 5,
-               "gf_stage_kernel": 1}
-_DECODE_ONLY = ("decode_prep_kernel", "m1_prep_kernel", "scatter_recovered_kernel",
-                "rows_k1_kernel")
+               "gf_stage_kernel": 1, "gf_stream_kernel": 2}
+_DECODE_ONLY = ("decode_prep_kernel", "decode_prep_lane_kernel", "m1_prep_kernel",
+                "scatter_recovered_kernel", "rows_k1_kernel")
+
+
+def kernel_names(k, m, bb):
+    """(encode, decode) kernel names the library picks for this shape (fec_api.cpp
+    encode_impl / decode_*_impl, gf_stream_supported, launch_decode_prep)."""
+    if m == 1:
+        return "xor_dma_kernel<encode>", "xor_dma_kernel<decode>"
+    rc = lambda n: min(1 << max(n - 1, 0).bit_length(), 8)
+    rmax = min(k, m)
+    stream = (bb == 1352 and (k * bb) % 16 == 0 and os.environ.get("QFEC_STREAM", "1") != "0")
+    enc = ("gf_stream_kernel<encode>" if stream and m <= rc(m) and
+           os.environ.get("QFEC_STREAM_ENC", "1") != "0" else "gf_apply_kernel<encode>")
+    lane = (rmax <= 4 and k <= 64 and k % 4 == 0 and m * k <= 4096 and
+            os.environ.get("QFEC_PREP_LANE", "1") != "0")
+    prep = "decode_prep_lane_kernel" if lane else "decode_prep_kernel"
+    dec = "gf_stream_kernel<decode>" if stream and rmax <= rc(rmax) else "gf_apply_kernel<decode>"
+    return enc, prep + " + " + dec
 
 
 def _phase(name):
@@ -303,12 +320,11 @@ def main():
     else:
         phase = "decode"
     traffic, traffic_src = pmc_traffic(args.workload, phase, G)
+    enc_kern, dec_kern = kernel_names(k, m, bb)
     if enc_ms >= dec_ms:
-        dom = ("encode", "xor_dma_kernel<encode>" if m == 1 else "gf_apply_kernel<encode>",
-               enc_gbs, enc_bytes)
+        dom = ("encode", enc_kern, enc_gbs, enc_bytes)
     else:
-        dom = ("decode", "xor_dma_kernel<decode>" if m == 1
-               else "decode_prep_kernel + gf_apply_kernel<decode>", dec_gbs, dec_bytes)
+        dom = ("decode", dec_kern, dec_gbs, dec_bytes)
 
     verified = None
     if args.verify:
