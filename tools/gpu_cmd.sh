@@ -1,5 +1,5 @@
 set -o pipefail
-mkdir -p gpurun_out/it9
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/it9/pytest.txt 2>&1 || { echo PYTEST_FAIL; tail -30 gpurun_out/it9/pytest.txt; exit 1; }
-timeout -k 10 120 python bench.py --workload B --no-cpu-baseline --no-host --steps 20 --verify > gpurun_out/it9/B.txt 2>&1 || exit 1
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/it9/prof -o run --output-format csv -- python bench.py --workload B --no-cpu-baseline --no-host --steps 10 > gpurun_out/it9/B_prof.txt 2>&1
+mkdir -p gpurun_out/it11
+for W in A B; do for E in 0 1; do
+QFEC_BENCH_NOEV=$E timeout -k 10 120 python bench.py --workload $W --no-cpu-baseline --no-host --steps 50 > gpurun_out/it11/${W}_noev$E.txt 2>&1 || exit 1
+done; done
