@@ -9,6 +9,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libquic_fec.so")
+# A/B experiments on one GPU box: QFEC_LIB_PATH names another build of the same library
+LIB_PATH = os.environ.get("QFEC_LIB_PATH", LIB_PATH)
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 
