@@ -134,7 +134,18 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
         sl = sl >= R ? sl - R : sl;
         const int idx = __builtin_amdgcn_readlane((int)vmv, sl);
         const int pending = vm - 1 - idx;
-        stream_wait_dyn<0, 63>(pending > 63 ? 63 : pending);
+        // coarse steps (a smaller count only waits longer): 4 scalar branch levels
+        if (pending >= 16) {
+            if (pending >= 32) {
+                if (pending >= 48) stream_wait_vmcnt<48>();
+                else stream_wait_vmcnt<32>();
+            } else {
+                if (pending >= 24) stream_wait_vmcnt<24>();
+                else stream_wait_vmcnt<16>();
+            }
+        } else {
+            stream_wait_dyn<0, 15>(pending < 0 ? 0 : pending);
+        }
     };
     // column word c of the 8 sub-rows as aligned dword pairs (the block start is 4-byte
     // aligned: slots are 1 KiB and BB % 8 == 0, so sub-row t is misaligned by the
@@ -199,7 +210,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                 expand_wz(v);
 #pragma unroll
                 for (int j = 0; j < RC; ++j) {
-                    if (j < n) {
+                    if (!DECODE && j == 0) {
+                        // encode row 0 is P0, all coefficients 1 (cauchy_256.cpp:1519-1523):
+                        // a plain XOR, no scalar nibble dispatch
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) acc[0][r] ^= v.W[r];
+                    } else if (j < n) {
                         const uint32_t cf = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
                         apply_nibble<0>(acc[j], cf & 15u, v);
                         apply_nibble<4>(acc[j], cf >> 4, v);
