@@ -71,7 +71,10 @@ constexpr int kStreamWaves = 4;            // waves per workgroup (independent)
 
 // S = sub-row bytes (bb / 8), compile-time so the 8 sub-row reads are one address + ds
 // offsets.  RC = outputs per group (one chunk: m <= RC for encode, rmax <= RC for decode).
-template <int RC, int S, bool DECODE>
+// RCPT = byte stride of a coefficient row in the table (max(4, table rc)).  Encode is
+// instantiated with RC = m exactly, so the per-output `j < n` test folds away (at run time
+// the compiler turned it into a lane mask: 2 VALU + 2 SALU per output and block).
+template <int RC, int S, bool DECODE, int RCPT = (RC < 4 ? 4 : RC)>
 __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
@@ -79,8 +82,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     constexpr int BB = 8 * S;
     constexpr int NW = (S + 3) / 4;                 // column words per sub-row
     constexpr int NWF = S / 4;                      // full words
-    constexpr int RCP = RC < 4 ? 4 : RC;
-    constexpr int NCW = RCP / 4;
+    constexpr int NCW = RCPT / 4;
+    static_assert(RCPT % 4 == 0 && RCPT >= RC, "coefficient row stride");
     constexpr int SPR = 1 + ((S >> 1) & 1) + (S & 1);   // store instructions per sub-row
     constexpr int SAUX = DECODE ? 0 : 2;   // encode's dense parity stream: nt stores
     static_assert(NW <= 64, "one column word per lane");
@@ -172,7 +175,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
 #pragma unroll 1
     for (long long i = 0; i < cnt; ++i) {
         const long long g = g0 + i * W;
-        int n = DECODE ? nout[g] : m;
+        int n = DECODE ? nout[g] : RC;   // encode: RC == m
         n = n > RC ? RC : n;
         if (n > 0) {
             const uint32_t* cw = (const uint32_t*)(coef + (DECODE ? g * coef_gstride : 0));
@@ -215,7 +218,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                         // a plain XOR, no scalar nibble dispatch
 #pragma unroll
                         for (int r = 0; r < 8; ++r) acc[0][r] ^= v.W[r];
-                    } else if (j < n) {
+                    } else if (!DECODE || j < n) {
                         const uint32_t cf = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
                         apply_nibble<0>(acc[j], cf & 15u, v);
                         apply_nibble<4>(acc[j], cf >> 4, v);
@@ -311,16 +314,31 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     if (const int lim = senv("QFEC_STREAM_GRID", 0)) cap = lim;   // tests: many groups per wave
     const unsigned grid = (unsigned)std::min<long long>(want, cap);
     const unsigned threads = kStreamWaves * 64;
-#define QS_GO(RCV, DEC)                                                                      \
-    hipLaunchKernelGGL((gf_stream_kernel<RCV, 169, DEC>), dim3(grid), dim3(threads), lds, st, \
-                       in, out, coef, slots, nout, groups, k, m, rmax, coef_gstride,          \
+#define QS_GO(RCV, DEC, RCPV)                                                                \
+    hipLaunchKernelGGL((gf_stream_kernel<RCV, 169, DEC, RCPV>), dim3(grid), dim3(threads), lds, \
+                       st, in, out, coef, slots, nout, groups, k, m, rmax, coef_gstride,       \
                        out_gstride, R)
     if (bb != 1352) return hipErrorInvalidValue;
-    switch (rc) {
-        case 2: if (decode) QS_GO(2, true); else QS_GO(2, false); break;
-        case 4: if (decode) QS_GO(4, true); else QS_GO(4, false); break;
-        case 8: if (decode) QS_GO(8, true); else QS_GO(8, false); break;
-        default: return hipErrorInvalidValue;
+    if (decode) {
+        switch (rc) {
+            case 2: QS_GO(2, true, 4); break;
+            case 4: QS_GO(4, true, 4); break;
+            case 8: QS_GO(8, true, 8); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        // one output per register set: RC = m; the table row stride is max(4, rc)
+        if ((rc < 4 ? 4 : rc) != (m <= 4 ? 4 : 8)) return hipErrorInvalidValue;
+        switch (m) {
+            case 2: QS_GO(2, false, 4); break;
+            case 3: QS_GO(3, false, 4); break;
+            case 4: QS_GO(4, false, 4); break;
+            case 5: QS_GO(5, false, 8); break;
+            case 6: QS_GO(6, false, 8); break;
+            case 7: QS_GO(7, false, 8); break;
+            case 8: QS_GO(8, false, 8); break;
+            default: return hipErrorInvalidValue;
+        }
     }
 #undef QS_GO
     return hipGetLastError();
