@@ -14,10 +14,10 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
             -mllvm -structurizecfg-skip-uniform-regions=true \
             -DQFEC_BUILD -DQFEC_TABLES_PATH='"$(TABLES)"' -Wall -Wno-unused-function
 
-SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_group.hip $(CSRC)/gf_stream.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp
+SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_group.hip $(CSRC)/gf_stream.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp $(CSRC)/fec_wire.cpp
 HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(CSRC)/gf_bitslice.h $(ROOT)include/quic_fec.h \
         $(ROOT)include/quic_fec_group.h $(ROOT)Makefile
-OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/xor_dma.o $(ROOT)build/gf_group.o $(ROOT)build/gf_stream.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o
+OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/xor_dma.o $(ROOT)build/gf_group.o $(ROOT)build/gf_stream.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o $(ROOT)build/fec_wire.o
 
 TOOL := $(ROOT)quic_amd/bin/fec_loopback
 
@@ -54,6 +54,10 @@ $(ROOT)build/fec_api.o: $(CSRC)/fec_api.cpp $(HDRS) $(TABLES)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(ROOT)build/fec_group.o: $(CSRC)/fec_group.cpp $(HDRS)
+	@mkdir -p $(ROOT)build
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(ROOT)build/fec_wire.o: $(CSRC)/fec_wire.cpp $(HDRS)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 

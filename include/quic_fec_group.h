@@ -101,6 +101,49 @@ QFEC_API int qfec_batch_poll(qfec_batch *b);    /* flushes if the timeout expire
 QFEC_API int qfec_batch_flush(qfec_batch *b);   /* >= 0 = groups processed */
 QFEC_API size_t qfec_batch_pending(const qfec_batch *b);
 
+/* ---- QuicR FEC wire format (the private part of the packet header + the FEC packet) ----
+ * What the framer adds to a QUIC packet for FEC (quic_framer.cc:850-893 write,
+ * :1219-1256 parse, :469-494 BuildFecPacket; flag bits quic_protocol.h:411-427):
+ *   private flags byte  bit 0 entropy, bit 1 FEC_GROUP, bit 2 FEC (payload is parity),
+ *                       bits 3..7 FecConfiguration (written as config << 3 into a byte)
+ *   FEC group offset    1 byte, packet_number - fec_group, only when FEC_GROUP is set
+ *   FEC packet          header bytes followed by the block_bytes parity block
+ * The public header before it (flags, connection id, version, nonce, packet number) is
+ * the QUIC stack's and out of scope; its size enters through qfec_wire_header_size. */
+typedef struct qfec_private_header {
+    unsigned long long packet_number;   /* write: this packet; read: from the public header */
+    unsigned long long fec_group;       /* first FEC-protected packet number (0 = none) */
+    int entropy_flag;
+    int fec_flag;                       /* payload is FEC redundancy */
+    int in_fec_group;
+    int fec_configuration;              /* FecConfiguration */
+} qfec_private_header;
+
+/* AppendPacketHeader's private part.  QUIC versions <= 33 write the flags byte a second
+ * time after the offset (quic_framer.cc:885-891, kept: the wire is the wire).  Returns the
+ * bytes written; -1 if in a group with fec_group > packet_number or an offset >= 255 (the
+ * reference's DCHECKs, :873-874); -2 if cap is too small. */
+QFEC_API int qfec_wire_write_private(const qfec_private_header *h, int quic_version,
+                                     unsigned char *out, size_t cap);
+/* ProcessAuthenticatedHeader.  h->packet_number must hold the packet number from the
+ * public header; the other fields are filled (0 when not in a group).  Returns the bytes
+ * consumed; -1 "Unable to read private flags", -2 "Unable to read first fec protected
+ * packet offset", -3 "First fec protected packet offset must be less than the packet
+ * number" (QUIC_INVALID_PACKET_HEADER in the reference). */
+QFEC_API int qfec_wire_read_private(const unsigned char *in, size_t len,
+                                    qfec_private_header *h);
+/* GetPacketHeaderSize (quic_protocol.cc:74-88): public flags + connection id + version
+ * (4) + path id (1) + packet number + diversification nonce (32) + FEC group offset (1,
+ * in a group) + private flags (1).  Also GetStartOfFecProtectedData with in_fec_group = 1. */
+QFEC_API size_t qfec_wire_header_size(int connection_id_length, int include_version,
+                                      int include_path_id, int include_nonce,
+                                      int packet_number_length, int in_fec_group);
+/* BuildFecPacket's body: header bytes then the redundancy block.  Returns the packet
+ * length, or -2 if cap is too small. */
+QFEC_API long qfec_wire_fec_packet(const unsigned char *header, size_t header_len,
+                                   const unsigned char *redundancy, size_t redundancy_len,
+                                   unsigned char *out, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

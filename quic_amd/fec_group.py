@@ -53,6 +53,11 @@ _SIG = {
     "qfec_batch_poll": (_c.c_int, [_c.c_void_p]),
     "qfec_batch_flush": (_c.c_int, [_c.c_void_p]),
     "qfec_batch_pending": (_c.c_size_t, [_c.c_void_p]),
+    "qfec_wire_write_private": (_c.c_int, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_size_t]),
+    "qfec_wire_read_private": (_c.c_int, [_c.c_char_p, _c.c_size_t, _c.c_void_p]),
+    "qfec_wire_header_size": (_c.c_size_t, [_c.c_int] * 6),
+    "qfec_wire_fec_packet": (_c.c_long, [_c.c_char_p, _c.c_size_t, _c.c_char_p, _c.c_size_t,
+                                         _c.c_void_p, _c.c_size_t]),
 }
 _lib = None
 
@@ -209,3 +214,62 @@ class FecBatch:
 
     def pending(self):
         return self._L.qfec_batch_pending(self._h)
+
+
+# ---------------------------------------------------------------- FEC wire format
+class PrivateHeader(_c.Structure):
+    """qfec_private_header: the FEC fields of a QuicPacketHeader (quic_protocol.h:850-860)."""
+    _fields_ = [("packet_number", _c.c_ulonglong), ("fec_group", _c.c_ulonglong),
+                ("entropy_flag", _c.c_int), ("fec_flag", _c.c_int),
+                ("in_fec_group", _c.c_int), ("fec_configuration", _c.c_int)]
+
+
+def write_private(packet_number, fec_group=0, entropy_flag=False, fec_flag=False,
+                  in_fec_group=None, fec_configuration=FEC_OFF, quic_version=36):
+    """Private flags byte (+ FEC group offset) as AppendPacketHeader writes it
+    (quic_framer.cc:850-893).  in_fec_group defaults to fec_group != 0, as
+    QuicPacketCreator::FillPacketHeader sets it (quic_packet_creator.cc:784-788)."""
+    if in_fec_group is None:
+        in_fec_group = fec_group != 0
+    h = PrivateHeader(packet_number, fec_group, int(bool(entropy_flag)), int(bool(fec_flag)),
+                      int(bool(in_fec_group)), fec_configuration)
+    buf = (_c.c_uint8 * 4)()
+    n = lib().qfec_wire_write_private(_c.byref(h), quic_version, buf, 4)
+    if n < 0:
+        raise ValueError(f"qfec_wire_write_private: {n}")
+    return bytes(buf[:n])
+
+
+def read_private(data, packet_number):
+    """ProcessAuthenticatedHeader (quic_framer.cc:1219-1256): returns (fields dict, bytes
+    consumed); raises ValueError with the reference's error text on a bad header."""
+    h = PrivateHeader(packet_number, 0, 0, 0, 0, 0)
+    n = lib().qfec_wire_read_private(bytes(data), len(data), _c.byref(h))
+    if n < 0:
+        raise ValueError({-1: "Unable to read private flags.",
+                          -2: "Unable to read first fec protected packet offset.",
+                          -3: "First fec protected packet offset must be less than the "
+                              "packet number."}[n])
+    return ({"packet_number": h.packet_number, "fec_group": h.fec_group,
+             "entropy_flag": bool(h.entropy_flag), "fec_flag": bool(h.fec_flag),
+             "in_fec_group": bool(h.in_fec_group),
+             "fec_configuration": h.fec_configuration}, n)
+
+
+def header_size(connection_id_length, include_version, include_path_id, include_nonce,
+                packet_number_length, in_fec_group):
+    """GetPacketHeaderSize (quic_protocol.cc:74-88)."""
+    return lib().qfec_wire_header_size(connection_id_length, int(include_version),
+                                       int(include_path_id), int(include_nonce),
+                                       packet_number_length, int(in_fec_group))
+
+
+def fec_packet(header, redundancy):
+    """BuildFecPacket's body (quic_framer.cc:469-494): header bytes + parity block."""
+    n = len(header) + len(redundancy)
+    buf = (_c.c_uint8 * max(n, 1))()
+    r = lib().qfec_wire_fec_packet(bytes(header), len(header), bytes(redundancy),
+                                   len(redundancy), buf, n)
+    if r < 0:
+        raise ValueError(f"qfec_wire_fec_packet: {r}")
+    return bytes(buf[:r])
