@@ -10,19 +10,19 @@
 // that share one need barriers and an LDS reduction.
 //
 // Here every wave owns whole groups (g0, g0 + W, ...) and streams them through a private
-// LDS ring of R one-KiB slots, plus a 2 KiB mirror of slots 0 and 1 so that a block that
-// wraps round the ring end is still one contiguous read.  The wave consumes the blocks of a
+// LDS ring of R one-KiB slots (a block that wraps round the ring end is read with wrapped
+// per-lane addresses).  The wave consumes the blocks of a
 // group in order; before block x it tops the ring up with the next pieces of its stream
 // (crossing into its next group) and waits, with a counted `s_waitcnt vmcnt`, only for the
-// pieces block x covers.  No barriers, no cross-wave traffic, R - 4 pieces in flight per
-// wave (R = 8: 10 KiB of LDS per wave, 16 waves per CU).  Lane c takes column word c of the 8 sub-rows of block x with
+// pieces block x covers.  No barriers, no cross-wave traffic, about R - 4 pieces in flight
+// per wave (R = 10: 10 KiB of LDS per wave, 16 waves per CU).  Lane c takes column word c of the 8 sub-rows of block x with
 // unaligned ds_read_b32 (gfx950 unaligned LDS access), expands W/Z and applies the RC
 // outputs, exactly like gf_apply.  The group's outputs are stored when its last block is
 // done, through buffer stores whose out-of-range lanes are dropped, so the number of VMEM
 // instructions per group is fixed and the vmcnt bookkeeping is exact.
 //
-// vmcnt bookkeeping: `vm` counts every VMEM instruction the wave issued (DMA pieces, mirror
-// copies, stores); lane s of `vmv` holds the value of `vm` at the last instruction of the
+// vmcnt bookkeeping: `vm` counts every VMEM instruction the wave issued (DMA pieces and
+// stores); lane s of `vmv` holds the value of `vm` at the last instruction of the
 // piece now in slot s.  VMEM instructions retire in issue order, so waiting for
 // vmcnt <= vm - 1 - vmv[slot] retires that piece.  No other VMEM instruction may be
 // emitted in the loop (coefficients, nout and slots come through s_load); the ISA check
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const int lane = threadIdx.x & 63;
     const int w = wave_id();
     const int RB = R * 1024;
-    uint8_t* ring = smem + (size_t)w * (RB + 2048);
+    uint8_t* ring = smem + (size_t)w * RB;
     const long long W = (long long)gridDim.x * kStreamWaves;
     const long long g0 = (long long)blockIdx.x * kStreamWaves + w;
     if (g0 >= groups) return;
@@ -114,11 +114,6 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
         __builtin_amdgcn_global_load_lds(QS_GPTR(isrc + off), QS_LPTR(ring + iss_slot * 1024),
                                          16, 0, 2);
         ++vm;
-        if (iss_slot < 2) {                            // mirror of slots 0, 1 past the end
-            __builtin_amdgcn_global_load_lds(QS_GPTR(isrc + off),
-                                             QS_LPTR(ring + RB + iss_slot * 1024), 16, 0, 2);
-            ++vm;
-        }
         vmv = lane == iss_slot ? (uint32_t)(vm - 1) : vmv;
         ++issued;
         if (++iss_slot == R) iss_slot = 0;
@@ -152,16 +147,38 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     };
     // column word c of the 8 sub-rows as aligned dword pairs (the block start is 4-byte
     // aligned: slots are 1 KiB and BB % 8 == 0, so sub-row t is misaligned by the
-    // constant (t * S) & 3; v_alignbyte at use).  Reads past the ring end land in the
-    // mirror (< RB + 1.5 KiB).
+    // constant (t * S) & 3; v_alignbyte at use).  A block that ends at least 4 bytes
+    // before the ring end is read as it lies (ds_read2 pairs; the highest byte read is
+    // bp + BB + 3).  A block that wraps round the ring end (once per ring cycle) takes
+    // per-lane wrapped addresses, min(a, a - RB) in unsigned arithmetic, one dword at a
+    // time.  No mirror of the first slots is kept, so all R * 1 KiB of the wave's LDS are
+    // ring slots (R = 10 at 16 waves per CU, against 8 slots + 2 KiB mirror before).
     auto read_block = [&](uint32_t bp, uint32_t (&lo)[8], uint32_t (&hi)[8]) {
-        const uint8_t* L = ring + bp + 4u * (uint32_t)c;
+        if (bp + (uint32_t)BB + 4u <= (uint32_t)RB) {
+            const uint8_t* L = ring + bp + 4u * (uint32_t)c;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const int o = t * S;
-            const uint32_t* q = (const uint32_t*)(L + (o & ~3));
-            lo[t] = q[0];
-            hi[t] = (o & 3) ? q[1] : 0u;
+            for (int t = 0; t < 8; ++t) {
+                const int o = t * S;
+                const uint32_t* q = (const uint32_t*)(L + (o & ~3));
+                lo[t] = q[0];
+                hi[t] = (o & 3) ? q[1] : 0u;
+            }
+        } else {
+            const uint32_t base = bp + 4u * (uint32_t)c;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int o = t * S;
+                const uint32_t a0 = base + (uint32_t)(o & ~3);
+                const uint32_t w0 = min(a0, a0 - (uint32_t)RB);
+                lo[t] = *(const uint32_t*)(ring + w0);
+                if (o & 3) {
+                    const uint32_t a1 = a0 + 4u;
+                    const uint32_t w1 = min(a1, a1 - (uint32_t)RB);
+                    hi[t] = *(const uint32_t*)(ring + w1);
+                } else {
+                    hi[t] = 0u;
+                }
+            }
         }
     };
     auto next_pos = [&](uint32_t bp) -> uint32_t {
@@ -283,7 +300,7 @@ int stream_cus() {
 }
 
 int stream_ring() {
-    const int r = senv("QFEC_STREAM_RING", 8);
+    const int r = senv("QFEC_STREAM_RING", 10);
     return r < 4 ? 4 : (r > 36 ? 36 : r);
 }
 
@@ -306,7 +323,7 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     if (groups <= 0) return hipSuccess;
     if (((uintptr_t)in & 15) != 0 || ((uintptr_t)slots & 3) != 0) return hipErrorInvalidValue;
     const int R = stream_ring();
-    const size_t lds = (size_t)kStreamWaves * (R + 2) * 1024;
+    const size_t lds = (size_t)kStreamWaves * R * 1024;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int per_cu = (int)((160 * 1024) / lds);
     const long long want = (groups + kStreamWaves - 1) / kStreamWaves;
