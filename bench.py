@@ -5,28 +5,34 @@ One step = one encode of a batch of packet groups (data -> parity) plus one deco
 receive set of the same batch (the first k packets that arrived, r data blocks lost per
 group, recovered out of place), all inputs resident in HBM before timing starts.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload A|B|D] [--groups G]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload A|B|C|D] [--groups G]
+  torchrun --nproc-per-node N bench.py --gpus N ...      (N > 1: one rank per GPU)
 
 Workloads (BASELINE.json configs):
-  A  65,536 groups of (10 data + 1 XOR parity) x 1350 B payloads, 1-loss decode  [default]
+  A  65,536 groups of (10 data + 1 XOR parity) x 1350 B, 1-loss decode   [default, N = 1]
   B  65,536 groups of (32 + 4) x 1350 B, GF(2^8) encode + 2-loss decode
+  C  1,048,576 groups of (32 + 4) x 1350 B split over the N GPUs (strong scaling),
+     per-GPU and aggregate rates                                           [default, N > 1]
   D  65,536 groups of (128 + 16) x 9000 B jumbo, GF(2^8) encode + 8-loss decode
 Each 1350 B payload travels as a block_bytes = roundup8(1350 + 2) = 1352 B block
 (2-byte length prefix, quic_fec_group.cc:109-121,344-352); jumbo 9000 B -> 9008 B.
 
-Multi-GPU (torchrun, one rank per GPU): groups are independent, so every rank runs its
-own contiguous shard of the same size (weak scaling) with no collective on the data
-path; a barrier brackets the timed region and the max time over ranks is reported.
+Multi-GPU: groups are independent, so every rank runs its own contiguous range of the
+global workload (A/B/D: G per rank, weak scaling; C: a 1/N share of 1,048,576 groups,
+strong scaling) with no collective on the data path; a barrier brackets the timed
+region and the max time over ranks is reported.
 
 value  = goodput = total groups * k * payload_bytes / step time, GiB/s
 roofline: the dominant kernel's algorithmic HBM bytes per launch / its mean launch time
 (HIP events on the launch stream), against the 8.0 TB/s HBM3E peak.
 cpu_baseline: the reference codec (oracle/_ref, compiled from the reference's own
-sources) or the oracle port, timed on this host's cores over a bounded sample.
+sources) or the oracle port, timed on this host's cores over a bounded sample, 1 thread
+and one thread per core of this process's CPU share.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -35,13 +41,15 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# name: (k, m, payload, losses r, groups, strong)  groups = per GPU (weak) or total (strong)
 WORKLOADS = {
-    # name: (k, m, payload, r, label)
-    "A": (10, 1, 1350, 1, "65536 x (10+1) x 1350B XOR parity, 1-loss decode"),
-    "B": (32, 4, 1350, 2, "65536 x (32+4) x 1350B GF(2^8), 2-loss decode"),
-    "D": (128, 16, 9000, 8, "65536 x (128+16) x 9000B GF(2^8), 8-loss decode"),
+    "A": (10, 1, 1350, 1, 65536, False),
+    "B": (32, 4, 1350, 2, 65536, False),
+    "C": (32, 4, 1350, 2, 1048576, True),
+    "D": (128, 16, 9000, 8, 65536, False),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+METRIC = "device-resident FEC encode+decode GiB/s over 1350B-payload packet groups"
 
 
 def block_bytes(payload):
@@ -49,38 +57,112 @@ def block_bytes(payload):
     return bb + (-bb) % 8
 
 
+def workload_label(name, k, m, payload, r, groups_total, world):
+    kind = "XOR parity" if m == 1 else "GF(2^8)"
+    lab = f"{groups_total} x ({k}+{m}) x {payload}B {kind}, {r}-loss decode"
+    if world > 1:
+        lab += f", {world} GPUs"
+    return f"{name}: {lab}"
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_share():
+    """Cores this process may use (the GPU box gives one GPU's job a share of the host;
+    nproc shows the whole machine), capped at 16 as the box's CPU share."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+def cpu_codec_rate(k, m, bb, payload, data_h, blocks_h, rows_h, seconds, threads, use_ref):
+    """Time only the codec calls: encode into a preallocated parity buffer, decode in place
+    on a fresh copy of the receive set made before its timer starts."""
+    from oracle import oracle as O
+    G = data_h.shape[0]
+    parity = np.zeros((G, m, bb), np.uint8)
+    work = np.empty_like(blocks_h)
+    wrows = np.empty_like(rows_h)
+    status = np.zeros(G, np.int32)
+    t_enc = t_dec = 0.0
+    passes = 0
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < seconds or passes == 0:
+        t0 = time.perf_counter()
+        O.encode_into(k, m, bb, data_h, parity, threads=threads, use_ref=use_ref)
+        t1 = time.perf_counter()
+        np.copyto(work, blocks_h)
+        np.copyto(wrows, rows_h)
+        t2 = time.perf_counter()
+        O.decode_inplace(k, m, bb, work, wrows, status, threads=threads, use_ref=use_ref)
+        t3 = time.perf_counter()
+        t_enc += t1 - t0
+        t_dec += t3 - t2
+        passes += 1
+    gib = passes * G * k * payload / 2**30
+    assert int(np.abs(status).max()) == 0
+    return {"value": round(gib / (t_enc + t_dec), 4), "threads": threads, "passes": passes,
+            "encode_GiBps": round(gib / t_enc, 3), "decode_GiBps": round(gib / t_dec, 3),
+            "encode_s": round(t_enc, 3), "decode_s": round(t_dec, 3)}
+
+
 def cpu_baseline(k, m, bb, payload, r, data_h, blocks_h, rows_h, seconds):
-    """Time the CPU codec on a bounded host sample (1 thread)."""
+    """The CPU FEC path on this host: one thread, and one thread per core of the share."""
     from oracle import oracle as O
     use_ref = O.ref_available()
     kind = "reference" if use_ref else "port"
-    G = data_h.shape[0]
-    t_enc = t_dec = 0.0
-    groups_done = 0
-    t_start = time.perf_counter()
-    while time.perf_counter() - t_start < seconds or groups_done == 0:
-        t0 = time.perf_counter()
-        O.encode_batch(k, m, bb, data_h, threads=1, use_ref=use_ref)
-        t1 = time.perf_counter()
-        b = blocks_h.copy()
-        t2 = time.perf_counter()
-        O.decode_batch(k, m, bb, b, rows_h, threads=1, use_ref=use_ref)
-        t3 = time.perf_counter()
-        t_enc += t1 - t0
-        t_dec += t3 - t2   # (decode_batch copies its inputs: included, a few % at most)
-        groups_done += G
-    gib = groups_done * k * payload / 2**30
+    n = cpu_share()
+    G = data_h.shape[0] // n          # per-thread sample; the n-thread leg runs n of them
+    one = cpu_codec_rate(k, m, bb, payload, data_h[:G], blocks_h[:G], rows_h[:G],
+                         seconds * 0.6, 1, use_ref)
+    many = cpu_codec_rate(k, m, bb, payload, data_h, blocks_h, rows_h, seconds * 0.4, n,
+                          use_ref) if n > 1 else one
     return {
-        "value": round(gib / (t_enc + t_dec), 4),
+        "value": many["value"],
         "unit": "GiB/s",
-        "cores": 1,
+        "cores": n,
         "kind": kind,
-        "sample": f"{G} groups x {groups_done // G} passes of the same workload "
-                  f"(encode + {r}-loss decode), host memory, 1 thread, "
+        "cpu_model": cpu_model(),
+        "sample": f"{G} groups per thread ({n * G} for {n} threads) of the same workload, "
+                  f"encode + {r}-loss decode in place, host memory, codec calls only "
+                  f"(receive-set copies outside the timer), "
                   f"{'oracle/_ref (reference libcat codec)' if use_ref else 'oracle port'}",
-        "encode_s": round(t_enc, 3),
-        "decode_s": round(t_dec, 3),
+        "threads_n": many,
+        "threads_1": one,
     }
+
+
+def loopback_config0():
+    """BASELINE.json configs[0]: one FEC group of 10 x 1350 B payloads, XOR parity encode +
+    1-loss recover through the loopback tool with the GPU off (the reference codec as
+    the --cpu-codec library).  Returns the tool's JSON line with codec times in us."""
+    tool = os.path.join(ROOT, "quic_amd", "bin", "fec_loopback")
+    from oracle import oracle as O
+    if not (os.path.exists(tool) and O.ref_available()):
+        return None
+    cmd = [tool, f"--cpu-codec={O.REF_SO}", "--fec", "--m=10", "--k=1", "--bytes=13500",
+           "--drop=4", "--port=0"]
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=60)
+        d = json.loads(out.stdout.strip().splitlines()[-1])
+    except Exception as e:   # the bench line still prints; the failure is reported
+        return {"error": repr(e)}
+    return {"config": "BASELINE configs[0]: 1 group of 10 x 1350 B, XOR parity, packet 4 "
+                      "dropped, loopback UDP, reference codec on the CPU",
+            "match": d.get("match"), "revived": d.get("revived"),
+            "encode_us": round(d["encode_s"] * 1e6, 2), "decode_us": round(d["decode_s"] * 1e6, 2),
+            "wall_s": d.get("wall_s")}
 
 
 # Which template argument of each kernel says "decode" (bool): the PMC summaries are split
@@ -89,7 +171,6 @@ _DECODE_ARG = {"xor_dma_kernel": 2, "gf_apply_kernel": 1, "gf_ring_kernel": 5,
                "gf_stage_kernel": 1, "gf_stream_kernel": 2}
 _DECODE_ONLY = ("decode_prep_kernel", "decode_prep_lane_kernel", "m1_prep_kernel",
                 "scatter_recovered_kernel", "rows_k1_kernel")
-
 
 
 class DeviceEvents:
@@ -126,7 +207,7 @@ class DeviceEvents:
             self.ev.append(e)
 
     def record(self, i, stream):
-        if self._hip.hipEventRecord(self.ev[i], ctypes_stream(stream)) != 0:
+        if self._hip.hipEventRecord(self.ev[i], self._ct.c_void_p(stream.cuda_stream)) != 0:
             raise RuntimeError("hipEventRecord failed")
 
     def elapsed_ms(self, i, j):
@@ -139,27 +220,6 @@ class DeviceEvents:
         for e in self.ev:
             self._hip.hipEventDestroy(e)
         self.ev = []
-
-
-def ctypes_stream(stream):
-    import ctypes
-    return ctypes.c_void_p(stream.cuda_stream)
-
-def kernel_names(k, m, bb):
-    """(encode, decode) kernel names the library picks for this shape (fec_api.cpp
-    encode_impl / decode_*_impl, gf_stream_supported, launch_decode_prep)."""
-    if m == 1:
-        return "xor_dma_kernel<encode>", "xor_dma_kernel<decode>"
-    rc = lambda n: min(1 << max(n - 1, 0).bit_length(), 8)
-    rmax = min(k, m)
-    stream = (bb == 1352 and (k * bb) % 16 == 0 and os.environ.get("QFEC_STREAM", "1") != "0")
-    enc = ("gf_stream_kernel<encode>" if stream and m <= rc(m) and
-           os.environ.get("QFEC_STREAM_ENC", "1") != "0" else "gf_apply_kernel<encode>")
-    lane = (rmax <= 4 and k <= 64 and k % 4 == 0 and m * k <= 4096 and
-            os.environ.get("QFEC_PREP_LANE", "1") != "0")
-    prep = "decode_prep_lane_kernel" if lane else "decode_prep_kernel"
-    dec = "gf_stream_kernel<decode>" if stream and rmax <= rc(rmax) else "gf_apply_kernel<decode>"
-    return enc, prep + " + " + dec
 
 
 def _phase(name):
@@ -236,6 +296,7 @@ def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps, recovered)
     return {
         "value": round(G * k * payload / 2**30 / ((t_enc + t_dec) / steps), 3),
         "unit": "GiB/s",
+        "groups": G,
         "encode_ms": round(t_enc / steps * 1e3, 3),
         "decode_ms": round(t_dec / steps * 1e3, 3),
         "pcie_bytes_per_step": pcie,
@@ -250,33 +311,49 @@ def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps, recovered)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= WORLD_SIZE; N > 1 runs under torchrun, one rank per GPU)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="A", choices=sorted(WORKLOADS))
-    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-groups", type=int, default=4096)
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: A on one GPU, C (strong scaling over 1,048,576 groups) "
+                         "on several")
+    ap.add_argument("--groups", type=int, default=None,
+                    help="groups per GPU (A/B/D) or in total (C); default: the BASELINE size")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-groups", type=int, default=None,
+                    help="groups per thread in the CPU sample (default: about 8 MB of data "
+                         "blocks, so the reference's working set stays cache-resident as on "
+                         "the QUIC thread)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check recovered data after timing")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) leg")
+    ap.add_argument("--host-groups", type=int, default=None,
+                    help="groups in the host-inclusive leg (default: all, at most 4 GB)")
     ap.add_argument("--decode-layout", default="recovered", choices=["recovered", "slots"],
                     help="recovered: qfec_decode_batch_recovered writes the r recovered blocks "
                          "of each group densely (what the receiver consumes); slots: "
                          "qfec_decode_batch writes them into their slots of a [G][k][bb] "
                          "buffer (cauchy_256_decode layout, out of place)")
     ap.add_argument("--host-steps", type=int, default=3)
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine launch option (qfec_ctx_set_option), for A/B experiments")
     args = ap.parse_args()
-
-    import torch
-    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpus = world if args.gpus is None else args.gpus
+    if gpus != world:
+        sys.exit(f"--gpus {gpus} but WORLD_SIZE={world}: launch N > 1 GPUs with "
+                 f"`torchrun --nproc-per-node {gpus} bench.py --gpus {gpus}`")
+
+    import torch
+    import torch.distributed as dist
+
     # QFEC_BENCH_BACKEND=gloo rehearses the N>1 control flow with several ranks sharing
     # one GPU (RCCL refuses two ranks on one device); the data path has no collective
-    # either way, only the barrier and the max-over-ranks of the elapsed time use it.
+    # either way, only the barrier, the max-over-ranks time and the per-rank report use it.
     backend = os.environ.get("QFEC_BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
     if world > 1 and backend == "gloo" and ndev > 0:
@@ -291,18 +368,27 @@ def main():
             dist.init_process_group(backend)
 
     from quic_amd import fec, shard, synth
-    k, m, payload, r, label = WORKLOADS[args.workload]
+    wname = args.workload or ("A" if world == 1 else "C")
+    k, m, payload, r, groups_dflt, strong = WORKLOADS[wname]
+    groups_arg = args.groups if args.groups is not None else groups_dflt
     bb = block_bytes(payload)
-    G = args.groups
+    if strong:
+        g0, G = shard.strong_range(groups_arg, world, rank)
+        total_groups = groups_arg
+    else:
+        g0, G = shard.weak_range(groups_arg, rank)
+        total_groups = groups_arg * world
     seed = 20251015
 
     eng = fec.FecEngine(local)
+    for o in args.opt:
+        name, val = o.split("=", 1)
+        eng.set_option(name, int(val))
     eng.reserve(k, m, bb, G)
     stream = torch.cuda.current_stream(dev)
 
-    # ---- resident inputs: this rank's shard [rank*G, (rank+1)*G) of the global workload
+    # ---- resident inputs: this rank's range [g0, g0 + G) of the global workload
     data = torch.empty((G, k, bb), dtype=torch.uint8, device=dev)
-    g0, _ = shard.weak_range(G, rank)
     fec.synth_fill(data, seed=seed, byte_offset=shard.data_byte_offset(g0, k, bb))
     parity = torch.zeros((G, m, bb), dtype=torch.uint8, device=dev)
     rc = eng.encode(k, m, bb, data, parity)
@@ -313,6 +399,7 @@ def main():
     src = torch.from_numpy(src_np).to(dev)
     blocks = torch.empty((G, k, bb), dtype=torch.uint8, device=dev)
     fec.synth_gather(data, parity, src, blocks, k, m, bb)
+    del src
     rmax = min(k, m)
     recovered = args.decode_layout == "recovered"
     if recovered:
@@ -324,16 +411,20 @@ def main():
     status = torch.zeros((G,), dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
 
+    kernels = {}
+
     def step(i=None):
         if i is not None:
             rec(3 * i)
         eng.encode(k, m, bb, data, parity)
+        kernels["encode"] = fec.last_kernels()
         if i is not None:
             rec(3 * i + 1)
         if recovered:
             eng.decode_recovered(k, m, bb, blocks, rows, out, rows_out, status=status)
         else:
             eng.decode(k, m, bb, blocks, rows, out=out, rows_out=rows_out, status=status)
+        kernels["decode"] = fec.last_kernels()
         if i is not None:
             rec(3 * i + 2)
 
@@ -370,12 +461,6 @@ def main():
     if dev_ev is not None:
         dev_ev.close()
 
-    elapsed = shard.max_over_ranks(elapsed, dev if backend == "nccl" else None)
-
-    ms_per_step = elapsed * 1e3 / args.steps
-    total_groups = G * world
-    goodput = shard.aggregate_goodput_gib(G, world, k, payload, elapsed / args.steps)
-
     # algorithmic HBM bytes per launch: encode reads k, writes m blocks;
     # decode reads the k received blocks and writes the r recovered ones
     enc_bytes = G * (k + m) * bb
@@ -383,16 +468,27 @@ def main():
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
     step_gbs = (enc_bytes + dec_bytes) / (enc_ms + dec_ms) / 1e6
-    if enc_ms >= dec_ms:
-        phase = "encode"
+    mine = {"rank": rank, "device": local, "groups": G, "first_group": g0,
+            "wall_ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+            "GiBps": round(G * k * payload / 2**30 / (elapsed / args.steps), 3),
+            "encode_ms": round(enc_ms, 5), "decode_ms": round(dec_ms, 5),
+            "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4)}
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     else:
-        phase = "decode"
-    traffic, traffic_src = pmc_traffic(args.workload, phase, G)
-    enc_kern, dec_kern = kernel_names(k, m, bb)
-    if enc_ms >= dec_ms:
-        dom = ("encode", enc_kern, enc_gbs, enc_bytes)
+        per_rank = [mine]
+
+    elapsed = shard.max_over_ranks(elapsed, dev if backend == "nccl" else None)
+    ms_per_step = elapsed * 1e3 / args.steps
+    goodput = total_groups * k * payload / 2**30 / (elapsed / args.steps)
+
+    phase = "encode" if enc_ms >= dec_ms else "decode"
+    traffic, traffic_src = pmc_traffic("B" if wname == "C" else wname, phase, G)
+    if phase == "encode":
+        dom = (kernels["encode"], enc_gbs, enc_bytes, enc_ms)
     else:
-        dom = ("decode", dec_kern, dec_gbs, dec_bytes)
+        dom = (kernels["decode"], dec_gbs, dec_bytes, dec_ms)
 
     verified = None
     if args.verify:
@@ -407,21 +503,28 @@ def main():
             g_idx = torch.arange(G, device=dev)[:, None].expand(G, k)[slot]
             verified = bool(torch.equal(out[slot], data[g_idx, rows_out.long()[slot]]))
         verified = verified and int(status.abs().max()) == 0
+        if world > 1:
+            flags = [None] * world
+            dist.all_gather_object(flags, verified)
+            verified = all(flags)
 
     cpu = None
+    cfg0 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        n = min(args.cpu_groups, G)
+        n = min((args.cpu_groups or max(16, (8 << 20) // (k * bb))) * cpu_share(), G)
         cpu = cpu_baseline(k, m, bb, payload, r, data[:n].cpu().numpy(),
                            blocks[:n].cpu().numpy(), rows_np[:n], args.cpu_seconds)
+        cfg0 = loopback_config0()
 
     host = None
     if rank == 0 and world == 1 and not args.no_host:
-        host = host_inclusive(eng, k, m, bb, payload, data, blocks, rows, args.host_steps,
-                              recovered)
+        hg = args.host_groups or max(1, min(G, (4 << 30) // (2 * k * bb)))
+        host = host_inclusive(eng, k, m, bb, payload, data[:hg], blocks[:hg], rows[:hg],
+                              args.host_steps, recovered)
 
     if rank == 0:
         line = {
-            "metric": "device-resident FEC encode+decode GiB/s over 1350B-payload packet groups",
+            "metric": METRIC,
             "value": round(goodput, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -429,39 +532,45 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded splitmix64 payload bytes, random per-group loss "
                     "patterns); device-resident",
             "config": {
-                "workload": label,
+                "workload": workload_label(wname, k, m, payload, r, total_groups, world),
                 "groups_per_gpu": G,
                 "groups_total": total_groups,
                 "k": k, "m": m, "payload_bytes": payload, "block_bytes": bb,
                 "losses_per_group": r,
                 "parallelism": f"{world} independent group shards (no collective)",
                 "decode_layout": args.decode_layout,
+                "options": args.opt,
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": dom[1],
-                "achieved": round(dom[2], 1),
+                "kernel": dom[0],
+                "phase": phase,
+                "achieved": round(dom[1], 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(dom[2] / HBM_PEAK_GBS, 4),
+                "frac": round(dom[1] / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": dom[3],
+                "algorithmic_bytes_per_launch": dom[2],
+                "launch_ms": round(dom[3], 5),
                 "timing": event_kind + " pairs around each launch, launch stream, timed steps",
             },
             "kernels": {
+                "encode": kernels["encode"], "decode": kernels["decode"],
                 "encode_ms": round(enc_ms, 5), "encode_GBps": round(enc_gbs, 1),
                 "decode_ms": round(dec_ms, 5), "decode_GBps": round(dec_gbs, 1),
                 "step_GBps": round(step_gbs, 1),
                 "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4),
             },
+            "per_gpu": per_rank,
             "cpu_baseline": cpu,
+            "cpu_reference_config0": cfg0,
             "host_inclusive": host,
         }
         if verified is not None:

@@ -65,11 +65,28 @@ QFEC_API int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes);
  *   status [G]          per-group return code of the equivalent cauchy_256_decode call
  * `stream` is a hipStream_t (NULL = HIP's null stream, as everywhere in HIP).  Device
  * entry points only enqueue work on that stream; they do not synchronise.
+ *
+ * Streams and contexts: a context may be used from several streams.  Its decode
+ * workspace is shared by its calls, so the library orders a decode behind the previous
+ * decode of the same context when they are enqueued on different streams (an event, not
+ * a host wait); calls on one stream are ordered by the stream.  Independent contexts
+ * (one per stream, or one per device) share nothing and run concurrently.  While a
+ * stream is capturing into a HIP graph the cross-stream ordering is not added: capture
+ * the calls of one context on one stream.  Calls on one context are serialised on the
+ * host by a mutex (the reference codec is single-threaded per connection).
  * ------------------------------------------------------------------------------- */
 typedef struct qfec_ctx qfec_ctx;
 
 QFEC_API int qfec_ctx_create(int device, qfec_ctx **out);
 QFEC_API void qfec_ctx_destroy(qfec_ctx *ctx);
+/* Launch-shape options of one context (the defaults are the measured best):
+ * "xor_slots" 2..4, "xor_waves" 1..4, "dma" 0/1, "stream" 0/1, "stream_ring" 4..36,
+ * "stream_grid" 0.., "pd" 1..3, "flat" 0/1, "enc_rc" 2/4/8, "prep_lane" 0/1,
+ * "host_chunk_mb" 1..4096.  get also reads "cus" (compute units of the device).
+ * -2 for an unknown name or a value out of range.  No environment variable changes
+ * what the library launches. */
+QFEC_API int qfec_ctx_set_option(qfec_ctx *ctx, const char *name, int value);
+QFEC_API int qfec_ctx_get_option(qfec_ctx *ctx, const char *name, int *value);
 /* Pre-size every per-(k, m) table and workspace for up to `groups` groups so that later
  * calls allocate nothing (required before capturing calls into a HIP graph). */
 QFEC_API int qfec_reserve(qfec_ctx *ctx, int k, int m, int block_bytes, long long groups);
@@ -128,6 +145,9 @@ QFEC_API int qfec_synth_gather(const unsigned char *d_data, const unsigned char 
                       int block_bytes, long long groups, void *stream);
 
 QFEC_API const char *qfec_last_error(void);
+/* Names of the kernels this thread's last engine call launched, " + "-separated, e.g.
+ * "decode_prep_lane_kernel + gf_stream_kernel<decode>" (bench.py reports it). */
+QFEC_API const char *qfec_last_kernels(void);
 QFEC_API int qfec_version(void);
 
 #ifdef __cplusplus

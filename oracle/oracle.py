@@ -136,6 +136,29 @@ def decode_batch(k, m, bb, blocks, rows, threads=1, use_ref=False):
     return blocks, rows, status
 
 
+def encode_into(k, m, bb, data, parity, threads=1, use_ref=False):
+    """Encode data [G][k][bb] into the caller's parity [G][m][bb] (no copies; for timing)."""
+    L = lib()
+    G = data.shape[0]
+    if use_ref:
+        fn = ctypes.cast(ref().cauchy_256_encode, ctypes.c_void_p)
+        return L.oracle_run_encode_batch(fn, k, m, bb, G, _ptr(data), _ptr(parity), threads)
+    return L.oracle_encode_batch(k, m, bb, G, _ptr(data), _ptr(parity), threads)
+
+
+def decode_inplace(k, m, bb, blocks, rows, status, threads=1, use_ref=False):
+    """Decode the caller's blocks [G][k][bb] / rows [G][k] in place (no copies; for
+    timing).  status: int32 [G]."""
+    L = lib()
+    G = blocks.shape[0]
+    if use_ref:
+        fn = ctypes.cast(ref().cauchy_256_decode, ctypes.c_void_p)
+        L.oracle_run_decode_batch(fn, k, m, bb, G, _ptr(blocks), _ptr(rows), _ptr(status),
+                                  threads)
+    else:
+        L.oracle_decode_batch(k, m, bb, G, _ptr(blocks), _ptr(rows), _ptr(status), threads)
+
+
 def encode_ptrs(k, m, bb, blocks, use_ref=False):
     """Single-group call through the cauchy_256 ABI with a pointer array
     (blocks: list of k uint8 arrays of bb bytes).  Returns (recovery [m][bb], rc)."""

@@ -60,7 +60,11 @@ SIGNATURES = {
     "qfec_synth_gather": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p]),
+    "qfec_ctx_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
+    "qfec_ctx_get_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p,
+                                           ctypes.POINTER(ctypes.c_int)]),
     "qfec_last_error": (ctypes.c_char_p, []),
+    "qfec_last_kernels": (ctypes.c_char_p, []),
     "qfec_version": (ctypes.c_int, []),
 }
 

@@ -48,6 +48,7 @@ enum {
 };
 
 thread_local std::string g_err;
+thread_local std::string g_kernels;   // kernels launched by this thread's last call
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -97,14 +98,7 @@ int pow2_at_least(int v) {
     while (p < v) p <<= 1;
     return p;
 }
-int encode_rc(int m) {
-    static const int cap = [] {
-        const char* e = getenv("QFEC_ENC_RC");   // 2, 4 or 8 (tuning)
-        const int v = e ? atoi(e) : 8;
-        return (v == 2 || v == 4 || v == 8) ? v : 8;
-    }();
-    return std::min(pow2_at_least(m), cap);
-}
+int encode_rc(int m, const qfec::Tune& t) { return std::min(pow2_at_least(m), t.enc_rc); }
 int decode_rc(int rmax) { return std::min(pow2_at_least(rmax), 8); }
 
 struct DevBuf {
@@ -138,6 +132,13 @@ struct HostBuf {
 struct qfec_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    qfec::Tune tune;
+    // The decode workspace (dcoef, dslots, dnout, dscratch) is one per context.  Calls may
+    // enqueue on any stream, so every use records ws_ev on its stream and a use on another
+    // stream first waits for it: uses of the workspace are ordered across streams.
+    hipEvent_t ws_ev = nullptr;
+    hipStream_t ws_stream = nullptr;
+    bool ws_used = false;
     // encode coefficient tables keyed by (k, m, rc): [nchunk][k][rcp]; decode cenc by (k, m)
     std::map<std::tuple<int, int, int>, std::unique_ptr<DevBuf>> enc_tab;
     std::map<std::pair<int, int>, std::unique_ptr<DevBuf>> cenc_tab;
@@ -156,7 +157,28 @@ struct qfec_ctx {
 namespace {
 
 int set_device(qfec_ctx* c) {
+    g_kernels.clear();
     QF_HIP(hipSetDevice(c->device));
+    return 0;
+}
+
+// Order this call's use of the context's decode workspace after the previous use (which
+// may have been enqueued on another stream).  Not while `st` is capturing into a graph:
+// there the calls of one capture are ordered by the capturing stream itself.
+int ws_begin(qfec_ctx* c, hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    QF_HIP(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone) return 0;
+    if (c->ws_used && c->ws_stream != st) QF_HIP(hipStreamWaitEvent(st, c->ws_ev, 0));
+    return 0;
+}
+int ws_end(qfec_ctx* c, hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    QF_HIP(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone) return 0;
+    QF_HIP(hipEventRecord(c->ws_ev, st));
+    c->ws_stream = st;
+    c->ws_used = true;
     return 0;
 }
 
@@ -231,31 +253,26 @@ int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     // m > 1 with unsupported parameters the reference still writes it before
     // returning -1 (:1532-1534).
     if (m == 1 || k + m > 256 || bb % 8 != 0) {
-        QF_HIP(qfec::launch_xor_encode(d_data, d_par, k, bb, G, (long long)m * bb, st));
+        QF_HIP(qfec::launch_xor_encode(d_data, d_par, k, bb, G, (long long)m * bb, st, c->tune));
         return m == 1 ? 0 : fail(-1, "unsupported (k + m > 256 or block_bytes % 8 != 0)");
     }
-    const int rc = encode_rc(m);
+    const int rc = encode_rc(m, c->tune);
     const uint8_t* tab = nullptr;
     int rcode = get_enc_table(c, k, m, rc, &tab);
     if (rcode) return rcode;
-    if (m <= rc && qfec::gf_stream_supported(k, m, bb, rc, false) && ((uintptr_t)d_data & 15) == 0) {
+    if (m <= rc && qfec::gf_stream_supported(k, m, bb, rc, false, c->tune) &&
+        ((uintptr_t)d_data & 15) == 0) {
         QF_HIP(qfec::launch_gf_stream(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc, 0, 0,
-                                      (long long)m * bb, false, st));
+                                      (long long)m * bb, false, st, c->tune));
         return 0;
     }
-    if (qfec::gf_group_supported(k, m, bb, rc)) {
-        QF_HIP(qfec::launch_gf_group(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc,
-                                     (m + rc - 1) / rc, 0, 0, (long long)m * bb, false, st));
-        return 0;
-    }
-    QF_HIP(qfec::launch_gf_encode(d_data, d_par, tab, k, m, bb, G, rc, st));
+    QF_HIP(qfec::launch_gf_encode(d_data, d_par, tab, k, m, bb, G, rc, st, c->tune));
     return 0;
 }
 
-int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d_blocks,
+int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d_blocks,
                 const uint8_t* d_rows_in, uint8_t* d_out, uint8_t* d_rows_out, int32_t* d_status,
                 hipStream_t st) {
-    if (G == 0) return 0;
     if (k <= 1) {   // cauchy_256.cpp:1257-1261
         QF_HIP(qfec::launch_rows_k1(d_rows_in, d_rows_out, d_status, G, st));
         return 0;
@@ -263,7 +280,7 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     if (m == 1) {   // :1264-1267
         QF_HIP(c->dslots.ensure((size_t)G));
         QF_HIP(qfec::launch_xor_decode(d_blocks, d_out, d_rows_in, d_rows_out, d_status,
-                                       (uint8_t*)c->dslots.p, k, bb, G, st));
+                                       (uint8_t*)c->dslots.p, k, bb, G, st, c->tune));
         return 0;
     }
     const int rmax = std::min(k, m);
@@ -275,23 +292,15 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
     qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
     QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc, rmax,
-                                    G, st));
+                                    G, st, c->tune));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
-    if (nchunk == 1 && qfec::gf_stream_supported(k, m, bb, rc, true) &&
+    if (nchunk == 1 && qfec::gf_stream_supported(k, m, bb, rc, true, c->tune) &&
         ((uintptr_t)d_blocks & 15) == 0) {
         // a group's stores follow all of its reads: in place needs no scratch
         const int rcp = std::max(rc, 4);
         QF_HIP(qfec::launch_gf_stream(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
                                       rmax, (long long)nchunk * k * rcp, (long long)k * bb, true,
-                                      st));
-        return 0;
-    }
-    if (qfec::gf_group_supported(k, m, bb, rc)) {
-        // whole group in LDS before any store: in place needs no scratch
-        const int rcp = std::max(rc, 4);
-        QF_HIP(qfec::launch_gf_group(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
-                                     nchunk, rmax, (long long)nchunk * k * rcp,
-                                     (long long)k * bb, true, st));
+                                      st, c->tune));
         return 0;
     }
     if (nchunk > 1 && d_out == d_blocks) {
@@ -299,13 +308,24 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
         // chunk already overwrote, so stage the recovered blocks first
         QF_HIP(c->dscratch.ensure((size_t)G * rmax * bb));
         QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, (uint8_t*)c->dscratch.p, w, k, m, bb, G,
-                                              rc, rmax, st));
+                                              rc, rmax, st, c->tune));
         QF_HIP(qfec::launch_scatter_recovered((const uint8_t*)c->dscratch.p, d_out, w, k, bb,
                                               rmax, G, st));
         return 0;
     }
-    QF_HIP(qfec::launch_gf_decode(d_blocks, d_out, w, k, m, bb, G, rc, rmax, st));
+    QF_HIP(qfec::launch_gf_decode(d_blocks, d_out, w, k, m, bb, G, rc, rmax, st, c->tune));
     return 0;
+}
+
+int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d_blocks,
+                const uint8_t* d_rows_in, uint8_t* d_out, uint8_t* d_rows_out, int32_t* d_status,
+                hipStream_t st) {
+    if (G == 0) return 0;
+    int r = ws_begin(c, st);
+    if (r) return r;
+    r = decode_body(c, k, m, bb, G, d_blocks, d_rows_in, d_out, d_rows_out, d_status, st);
+    const int r2 = ws_end(c, st);
+    return r ? r : r2;
 }
 
 // Recovered-blocks layout (qfec_decode_batch_recovered): the same decode, but recovered
@@ -313,10 +333,9 @@ int decode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
 // d_rec_rows[g * rmax + j] (ascending, 255 past the erasure count); blocks and row tags
 // are left as they are.  This is what the receiver consumes (getRevivedPackets,
 // quic_fec_group.cc:280-293, only extracts the missing packets), and the writes are dense.
-int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
+int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
                           const uint8_t* d_blocks, const uint8_t* d_rows_in, uint8_t* d_rec,
                           uint8_t* d_rec_rows, int32_t* d_status, hipStream_t st) {
-    if (G == 0) return 0;
     const int rmax = std::min(k, m);
     if (k <= 1) {
         QF_HIP(qfec::launch_rec_k1(d_blocks, d_rows_in, d_rec, d_rec_rows, d_status, bb, rmax, G,
@@ -326,7 +345,7 @@ int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
     if (m == 1) {
         QF_HIP(c->dslots.ensure((size_t)G));
         QF_HIP(qfec::launch_xor_decode(d_blocks, d_rec, d_rows_in, d_rec_rows, d_status,
-                                       (uint8_t*)c->dslots.p, k, bb, G, st, true));
+                                       (uint8_t*)c->dslots.p, k, bb, G, st, c->tune, true));
         return 0;
     }
     const int rc = decode_rc(rmax);
@@ -336,17 +355,31 @@ int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
     if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
     qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
     QF_HIP(qfec::launch_decode_prep(d_rows_in, nullptr, d_status, cenc, w, k, m, bb, rc, rmax, G,
-                                    st, d_rec_rows));
+                                    st, c->tune, d_rec_rows));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
-    if (rmax <= rc && qfec::gf_stream_supported(k, m, bb, rc, true) &&
+    if (rmax <= rc && qfec::gf_stream_supported(k, m, bb, rc, true, c->tune) &&
         ((uintptr_t)d_blocks & 15) == 0) {
         const int rcp = std::max(rc, 4);
         QF_HIP(qfec::launch_gf_stream(d_blocks, d_rec, w.coef, nullptr, w.nout, k, m, bb, G, rc,
-                                      rmax, (long long)k * rcp, (long long)rmax * bb, true, st));
+                                      rmax, (long long)k * rcp, (long long)rmax * bb, true, st,
+                                      c->tune));
         return 0;
     }
-    QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, d_rec, w, k, m, bb, G, rc, rmax, st));
+    QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, d_rec, w, k, m, bb, G, rc, rmax, st,
+                                          c->tune));
     return 0;
+}
+
+int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
+                          const uint8_t* d_blocks, const uint8_t* d_rows_in, uint8_t* d_rec,
+                          uint8_t* d_rec_rows, int32_t* d_status, hipStream_t st) {
+    if (G == 0) return 0;
+    int r = ws_begin(c, st);
+    if (r) return r;
+    r = decode_recovered_body(c, k, m, bb, G, d_blocks, d_rows_in, d_rec, d_rec_rows, d_status,
+                              st);
+    const int r2 = ws_end(c, st);
+    return r ? r : r2;
 }
 
 // Host-pointer batches, chunked and pipelined: chunk i's H2D (s_in), kernels (stream)
@@ -356,7 +389,7 @@ int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
 // never shared by two chunks in flight.  Chunk size: QFEC_HOST_CHUNK_MB (default 64).
 // fn(g0, n, buf, phase): phase 0 enqueues the H2D, 1 the kernels, 2 the D2H.
 template <class F>
-int host_pipeline(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
+int host_pipeline_body(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
     if (!c->s_in) {
         QF_HIP(hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking));
         QF_HIP(hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
@@ -366,8 +399,7 @@ int host_pipeline(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
             QF_HIP(hipEventCreateWithFlags(&c->ev_out[b], hipEventDisableTiming));
         }
     }
-    const char* e = getenv("QFEC_HOST_CHUNK_MB");
-    const size_t target = (size_t)(e && atoi(e) > 0 ? atoi(e) : 64) << 20;
+    const size_t target = (size_t)std::max(1, c->tune.host_chunk_mb) << 20;
     const long long chunk = std::max<long long>(1, std::min<long long>(groups, (long long)(target / per_group)));
     const size_t bytes = (size_t)chunk * per_group + 16;
     for (int b = 0; b < qfec_ctx::NB; ++b) QF_HIP(c->pbuf[b].ensure(bytes));
@@ -381,10 +413,7 @@ int host_pipeline(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
         if (r) return r;
         QF_HIP(hipEventRecord(c->ev_in[b], c->s_in));
         QF_HIP(hipStreamWaitEvent(c->stream, c->ev_in[b], 0));
-        if ((r = fn(g0, n, buf, 1))) {
-            (void)hipStreamSynchronize(c->s_out);
-            return r;
-        }
+        if ((r = fn(g0, n, buf, 1))) return r;
         QF_HIP(hipEventRecord(c->ev_done[b], c->stream));
         QF_HIP(hipStreamWaitEvent(c->s_out, c->ev_done[b], 0));
         if ((r = fn(g0, n, buf, 2))) return r;
@@ -394,7 +423,19 @@ int host_pipeline(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
     return 0;
 }
 
-// Default context for the single-group drop-ins (created on the caller's current device).
+// On any error, drain all three streams before returning, so no copy of an earlier chunk
+// still writes into the caller's host buffers after the call has returned.
+template <class F>
+int host_pipeline(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
+    const int r = host_pipeline_body(c, groups, per_group, fn);
+    if (r)
+        for (hipStream_t s : {c->s_in, c->stream, c->s_out})
+            if (s) (void)hipStreamSynchronize(s);
+    return r;
+}
+
+// Default context for the single-group drop-ins (created on the caller's current device;
+// QFEC_DEVICE names another, read once when the context is first needed).
 std::once_flag g_default_once;
 qfec_ctx* g_default = nullptr;
 int g_default_rc = 0;
@@ -413,12 +454,69 @@ int default_ctx(qfec_ctx** out) {
 
 }  // namespace
 
+namespace qfec {
+void note_kernel(const char* name) {
+    // a host-pointer batch launches the same kernels once per chunk: list each once
+    const std::string n(name);
+    size_t at = 0;
+    while ((at = g_kernels.find(n, at)) != std::string::npos) {
+        const size_t end = at + n.size();
+        if ((at == 0 || g_kernels.compare(at - 3, 3, " + ") == 0) &&
+            (end == g_kernels.size() || g_kernels.compare(end, 3, " + ") == 0))
+            return;
+        at = end;
+    }
+    if (!g_kernels.empty()) g_kernels += " + ";
+    g_kernels += n;
+}
+}  // namespace qfec
+
 // ======================================================================== C ABI
 extern "C" {
 
 int qfec_version(void) { return 1; }
 
 const char* qfec_last_error(void) { return g_err.c_str(); }
+
+const char* qfec_last_kernels(void) { return g_kernels.c_str(); }
+
+int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
+    if (!c || !name) return fail(-2, "null context or option name");
+    std::lock_guard<std::mutex> lk(c->mu);
+    struct Opt { const char* n; int* p; int lo, hi; };
+    qfec::Tune& t = c->tune;
+    const Opt opts[] = {
+        {"xor_slots", &t.xor_slots, 2, 4},     {"xor_waves", &t.xor_waves, 1, 4},
+        {"dma", &t.dma, 0, 1},                 {"stream", &t.stream, 0, 1},
+        {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
+        {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
+        {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
+        {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
+    };
+    for (const Opt& o : opts) {
+        if (strcmp(o.n, name) != 0) continue;
+        if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))))
+            return fail(-2, std::string("option value out of range: ") + name);
+        *o.p = value;
+        return 0;
+    }
+    return fail(-2, std::string("unknown option: ") + name);
+}
+
+int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
+    if (!c || !name || !value) return fail(-2, "null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    const qfec::Tune& t = c->tune;
+    const std::pair<const char*, int> opts[] = {
+        {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
+        {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
+        {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
+        {"host_chunk_mb", t.host_chunk_mb},
+    };
+    for (const auto& o : opts)
+        if (strcmp(o.first, name) == 0) { *value = o.second; return 0; }
+    return fail(-2, std::string("unknown option: ") + name);
+}
 
 int qfec_cauchy_matrix(int k, int m, unsigned char* out) {
     if (!blob_ok()) return fail(-2, "embedded Cauchy tables have the wrong size");
@@ -434,7 +532,11 @@ int qfec_ctx_create(int device, qfec_ctx** out) {
     auto c = std::make_unique<qfec_ctx>();
     c->device = device;
     QF_HIP(hipSetDevice(device));
+    int cus = 0;
+    QF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    c->tune.cus = cus > 0 ? cus : 256;
     QF_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    QF_HIP(hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming));
     *out = c.release();
     return 0;
 }
@@ -442,8 +544,10 @@ int qfec_ctx_create(int device, qfec_ctx** out) {
 void qfec_ctx_destroy(qfec_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->ws_used) (void)hipEventSynchronize(c->ws_ev);
     for (hipStream_t s : {c->stream, c->s_in, c->s_out})
         if (s) (void)hipStreamSynchronize(s);
+    if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
     for (int b = 0; b < qfec_ctx::NB; ++b)
         for (hipEvent_t e : {c->ev_in[b], c->ev_done[b], c->ev_out[b]})
             if (e) (void)hipEventDestroy(e);
@@ -702,7 +806,7 @@ int qfec_reserve(qfec_ctx* c, int k, int m, int bb, long long groups) {
     QF_HIP(c->dslots.ensure((size_t)groups));   // m == 1 decode: erased slot per group
     if (m > 1 && k > 1 && k + m <= 256) {
         const uint8_t* t;
-        if ((rc = get_enc_table(c, k, m, encode_rc(m), &t))) return rc;
+        if ((rc = get_enc_table(c, k, m, encode_rc(m, c->tune), &t))) return rc;
     }
     if (m > 1 && k > 1) {
         const uint8_t* t;

@@ -12,6 +12,27 @@
 
 namespace qfec {
 
+// Per-context launch configuration.  The defaults are the measured best shapes
+// (DESIGN.md); qfec_ctx_set_option() changes them for one context only, so no
+// environment variable can change what the product launches.
+struct Tune {
+    int cus = 256;            // compute units of the context's device (filled at create)
+    int xor_slots = 2;        // m = 1 LDS ring: group slots per wave (2..4)
+    int xor_waves = 3;        //                 waves per workgroup (1..4)
+    int dma = 1;              // m = 1: LDS-DMA ring kernel (0: flat register kernel)
+    int stream = 1;           // m > 1, small blocks: gf_stream (0: gf_apply)
+    int stream_ring = 10;     // gf_stream: 1 KiB ring slots per wave (4..36)
+    int stream_grid = 0;      // gf_stream: grid cap in workgroups (0: CUs x per-CU fit)
+    int pd = 2;               // gf_apply: register pipeline depth (1..3)
+    int flat = 1;             // gf_apply: lane-flat encode
+    int enc_rc = 8;           // gf_apply: encode outputs per wave (2, 4, 8)
+    int prep_lane = 1;        // decode prep with 4 lanes per group when it applies
+    int host_chunk_mb = 64;   // host-pointer batches: chunk size
+};
+
+// Records the name of a kernel a call launched (qfec_last_kernels(), per thread).
+void note_kernel(const char* name);
+
 // Decode work tables written by the prep kernel and read by the apply kernel.
 struct DecodeWork {
     uint8_t* coef;     // [G][nchunk][k][RCP]  bit-sliced GF(256) coefficients
@@ -22,14 +43,16 @@ struct DecodeWork {
 // parity[g*out_gstride ..+bb) = XOR of the k blocks of group g (m == 1 encode, and the
 // P0 the reference writes before rejecting invalid m > 1 parameters).
 hipError_t launch_xor_encode(const uint8_t* data, uint8_t* parity, int k, int bb,
-                             long long groups, long long out_gstride, hipStream_t st);
+                             long long groups, long long out_gstride, hipStream_t st,
+                             const Tune& t);
 
 // m == 1 decode: XOR the k-1 other blocks into the block tagged row >= k.  eidx is a
 // [G] byte workspace (erased slot per group).  compact: the recovered block of group g
 // goes to out + g * bb and its data row to rows_out[g] (255 = nothing erased).
 hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t* rows_in,
                              uint8_t* rows_out, int32_t* status, uint8_t* eidx, int k, int bb,
-                             long long groups, hipStream_t st, bool compact = false);
+                             long long groups, hipStream_t st, const Tune& t,
+                             bool compact = false);
 
 // k <= 1 encode: copy data[0] into each of the m outputs (cauchy_256.cpp:1508-1516).
 hipError_t launch_replicate(const uint8_t* data, uint8_t* parity, int m, int bb,
@@ -47,7 +70,8 @@ hipError_t launch_rows_k1(const uint8_t* rows_in, uint8_t* rows_out, int32_t* st
 // Bit-sliced GF(256) apply.  Encode: coef is the shared [nchunk][k][RCP] table built
 // from the Cauchy matrix (row 0 = ones), outputs are parity rows chunk*RC + j.
 hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t* coef,
-                            int k, int m, int bb, long long groups, int rc, hipStream_t st);
+                            int k, int m, int bb, long long groups, int rc, hipStream_t st,
+                            const Tune& t);
 
 // Decode prep: per group, sort blocks, invert the erasure submatrix in GF(256) and
 // emit the r x k recovery coefficients.  cenc is the [m][k] encode matrix (row 0 = ones).
@@ -56,43 +80,37 @@ hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t*
 hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
                               const uint8_t* cenc, DecodeWork w, int k, int m, int bb,
                               int rc, int rmax, long long groups, hipStream_t st,
-                              uint8_t* rec_rows = nullptr);
+                              const Tune& t, uint8_t* rec_rows = nullptr);
 
 // Decode apply: recovered block j of group g = sum_pos coef[g][..][pos][j] (x) blocks[g][pos],
 // written to out[g][slots[g][j]].
 hipError_t launch_gf_decode(const uint8_t* blocks, uint8_t* out, DecodeWork w, int k, int m,
-                            int bb, long long groups, int rc, int rmax, hipStream_t st);
+                            int bb, long long groups, int rc, int rmax, hipStream_t st,
+                            const Tune& t);
 
 // In-place decode when rmax > rc: apply into scratch [G][rmax][bb], then scatter to slots.
 hipError_t launch_gf_decode_scratch(const uint8_t* blocks, uint8_t* scratch, DecodeWork w,
                                    int k, int m, int bb, long long groups, int rc, int rmax,
-                                   hipStream_t st);
+                                   hipStream_t st, const Tune& t);
 hipError_t launch_scatter_recovered(const uint8_t* scratch, uint8_t* out, DecodeWork w, int k,
                                    int bb, int rmax, long long groups, hipStream_t st);
 
 // m = 1 LDS-ring XOR kernel (xor_dma.hip).  Requires 16-byte aligned `in`, 8-byte aligned
 // `out`/stride and bb % 8 == 0; decode with rows_in != null also does the row bookkeeping.
-bool xor_dma_ok(const void* in, const void* out, int k, int bb, long long ogs);
+bool xor_dma_ok(const void* in, const void* out, int k, int bb, long long ogs, const Tune& t);
 // compact: recovered-blocks layout (out [G][bb], rows_out [G] = recovered data row).
 hipError_t launch_xor_dma(const uint8_t* in, uint8_t* out, const uint8_t* eidx,
                           const uint8_t* rows_in, uint8_t* rows_out, int32_t* status, int k,
                           int bb, long long groups, long long out_gstride, bool decode,
-                          hipStream_t st, bool compact = false);
+                          hipStream_t st, const Tune& t, bool compact = false);
 
 // Per-wave LDS-ring streaming kernel for bb = 1352, one output chunk (gf_stream.hip).
-bool gf_stream_supported(int k, int m, int bb, int rc, bool decode);
+bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& t);
 hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef,
                             const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
                             long long groups, int rc, int rmax, long long coef_gstride,
-                            long long out_gstride, bool decode, hipStream_t st);
-
-// Whole-group LDS kernel for groups that fit in LDS (gf_group.hip).
-bool gf_group_supported(int k, int m, int bb, int rc);
-hipError_t launch_gf_group(const uint8_t* in, uint8_t* out, const uint8_t* coef,
-                           const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
-                           long long groups, int rc, int nchunk, int rmax,
-                           long long coef_gstride, long long out_gstride, bool decode,
-                           hipStream_t st);
+                            long long out_gstride, bool decode, hipStream_t st,
+                            const Tune& t);
 
 
 // Synthetic workload helpers (bench / tests): splitmix64 stream and receive-set gather.

@@ -888,26 +888,16 @@ static void xor_flat_launch(const uint8_t* in, uint8_t* out, const uint8_t* eidx
     }
 }
 
-static int num_cus() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            n <= 0)
-            n = 256;
-    }
-    return n;
-}
-
 template <bool DECODE>
 static hipError_t xor_any(const uint8_t* in, uint8_t* out, const uint8_t* eidx, int k, int bb,
                           long long G, long long igs, long long ogs, hipStream_t st,
-                          long long es = -1) {
+                          const Tune& t, long long es = -1) {
     if (es < 0) es = bb;
     if (G <= 0) return hipSuccess;
-    if (es == bb && igs == (long long)k * bb && xor_dma_ok(in, out, k, bb, ogs))
-        return launch_xor_dma(in, out, eidx, nullptr, nullptr, nullptr, k, bb, G, ogs, DECODE, st);
+    if (es == bb && igs == (long long)k * bb && xor_dma_ok(in, out, k, bb, ogs, t))
+        return launch_xor_dma(in, out, eidx, nullptr, nullptr, nullptr, k, bb, G, ogs, DECODE, st,
+                              t);
+    note_kernel(DECODE ? "xor_flat_kernel<decode>" : "xor_flat_kernel<encode>");
     const int vs = xor_unit(in, out, igs, ogs, bb);
     const long long units = G * ((bb + vs - 1) / vs);
     if (units > 0xffffffffLL) return hipErrorInvalidValue;
@@ -918,27 +908,29 @@ static hipError_t xor_any(const uint8_t* in, uint8_t* out, const uint8_t* eidx, 
 }
 
 hipError_t launch_xor_encode(const uint8_t* data, uint8_t* parity, int k, int bb,
-                             long long groups, long long out_gstride, hipStream_t st) {
+                             long long groups, long long out_gstride, hipStream_t st,
+                             const Tune& t) {
     return xor_any<false>(data, parity, nullptr, k, bb, groups, (long long)k * bb, out_gstride,
-                          st);
+                          st, t);
 }
 
 hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t* rows_in,
                              uint8_t* rows_out, int32_t* status, uint8_t* eidx, int k, int bb,
-                             long long groups, hipStream_t st, bool compact) {
+                             long long groups, hipStream_t st, const Tune& t, bool compact) {
     if (groups <= 0) return hipSuccess;
     const long long gb = (long long)k * bb;
     const long long ogs = compact ? bb : gb;
-    if (k <= 64 && xor_dma_ok(blocks, out, k, bb, ogs))
+    if (k <= 64 && xor_dma_ok(blocks, out, k, bb, ogs, t))
         // single launch: the DMA kernel also does the erased-slot / missing-row bookkeeping
         return launch_xor_dma(blocks, out, nullptr, rows_in, rows_out, status, k, bb, groups, ogs,
-                              true, st, compact);
+                              true, st, t, compact);
+    note_kernel("m1_prep_kernel");
     m1_prep_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(rows_in, rows_out, status,
                                                                      eidx, k, groups,
                                                                      compact ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return xor_any<true>(blocks, out, eidx, k, bb, groups, gb, ogs, st, compact ? 0 : bb);
+    return xor_any<true>(blocks, out, eidx, k, bb, groups, gb, ogs, st, t, compact ? 0 : bb);
 }
 
 hipError_t launch_replicate(const uint8_t* data, uint8_t* parity, int m, int bb,
@@ -946,6 +938,7 @@ hipError_t launch_replicate(const uint8_t* data, uint8_t* parity, int m, int bb,
     if (groups <= 0 || m <= 0) return hipSuccess;
     const long long total = groups * m * (long long)bb;
     const unsigned nb = (unsigned)std::min<long long>((total + 255) / 256, 65536);
+    note_kernel("replicate_kernel");
     replicate_kernel<<<nb, 256, 0, st>>>(data, parity, m, bb, groups);
     return hipGetLastError();
 }
@@ -956,6 +949,7 @@ hipError_t launch_rec_k1(const uint8_t* blocks, const uint8_t* rows_in, uint8_t*
     if (groups <= 0) return hipSuccess;
     const long long total = groups * (long long)bb;
     const unsigned nb = (unsigned)std::min<long long>((total + 255) / 256, 65536);
+    note_kernel("rec_k1_kernel");
     rec_k1_kernel<<<nb, 256, 0, st>>>(blocks, rows_in, rec, rec_rows, status, bb, rmax, groups);
     return hipGetLastError();
 }
@@ -963,30 +957,10 @@ hipError_t launch_rec_k1(const uint8_t* blocks, const uint8_t* rows_in, uint8_t*
 hipError_t launch_rows_k1(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
                           long long groups, hipStream_t st) {
     if (groups <= 0) return hipSuccess;
+    note_kernel("rows_k1_kernel");
     rows_k1_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(rows_in, rows_out, status,
                                                                      groups);
     return hipGetLastError();
-}
-
-// Register-pipeline depth of gf_apply_kernel (QFEC_PD=1|2|3 for experiments).
-static int pd_choice() {
-    static int pd = -1;
-    if (pd < 0) {
-        const char* e = getenv("QFEC_PD");
-        pd = e ? atoi(e) : 2;
-        if (pd < 1 || pd > 3) pd = 2;
-    }
-    return pd;
-}
-
-// Lane-flat encode (QFEC_FLAT=0 turns it off for experiments).
-static bool flat_choice() {
-    static int f = -1;
-    if (f < 0) {
-        const char* e = getenv("QFEC_FLAT");
-        f = e ? (atoi(e) != 0) : 1;
-    }
-    return f != 0;
 }
 
 template <bool DECODE>
@@ -994,11 +968,11 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
                                     const uint8_t* slots, const int32_t* nout, int k, int m,
                                     int bb, long long groups, int rc, int nchunk, int rmax,
                                     long long coef_gstride, long long out_gstride,
-                                    hipStream_t st) {
+                                    hipStream_t st, const Tune& t) {
     const int s = bb / 8;
     const int nw = (s + 3) / 4;
     const int ntiles = (nw + 63) / 64;
-    const bool flat = !DECODE && s >= 4 && flat_choice() && (nw & 63) != 0;
+    const bool flat = !DECODE && s >= 4 && t.flat && (nw & 63) != 0;
     const long long flat_lanes = groups * nw;
     const long long units = flat ? nchunk * ((flat_lanes + 63) / 64) : groups * nchunk * ntiles;
     if (units <= 0) return hipSuccess;
@@ -1006,7 +980,10 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
     const unsigned nb = blocks_for_waves(units);
     const unsigned nthr = 256;
     const int tu = (int)units;
-    const int pd = pd_choice();
+    const int pd = t.pd;
+    if (pd < 1 || pd > 3) return hipErrorInvalidValue;
+    note_kernel(DECODE ? "gf_apply_kernel<decode>"
+                       : (flat ? "gf_apply_kernel<encode,flat>" : "gf_apply_kernel<encode>"));
 #define QF_ARGS in, out, coef, slots, nout, k, m, bb, nw, ntiles, nchunk, rmax, coef_gstride, \
                 out_gstride, tu, flat_lanes
 #define QF_LAUNCH(RCV)                                                                        \
@@ -1037,22 +1014,24 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
 }
 
 hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t* coef, int k,
-                            int m, int bb, long long groups, int rc, hipStream_t st) {
+                            int m, int bb, long long groups, int rc, hipStream_t st,
+                            const Tune& t) {
     const int nchunk = (m + rc - 1) / rc;
     return gf_apply_dispatch<false>(data, parity, coef, nullptr, nullptr, k, m, bb, groups, rc,
-                                    nchunk, 0, 0, (long long)m * bb, st);
+                                    nchunk, 0, 0, (long long)m * bb, st, t);
 }
 
 hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
                               const uint8_t* cenc, DecodeWork w, int k, int m, int bb, int rc,
-                              int rmax, long long groups, hipStream_t st, uint8_t* rec_rows) {
+                              int rmax, long long groups, hipStream_t st, const Tune& t,
+                              uint8_t* rec_rows) {
     if (groups <= 0) return hipSuccess;
-    static const int lane_prep = getenv("QFEC_PREP_LANE") ? atoi(getenv("QFEC_PREP_LANE")) : 1;
-    if (lane_prep && rmax <= 4 && k <= 64 && k % 4 == 0 && (long long)m * k <= 4096 && rc <= 4 &&
+    if (t.prep_lane && rmax <= 4 && k <= 64 && k % 4 == 0 && (long long)m * k <= 4096 && rc <= 4 &&
         ((((uintptr_t)w.coef) | (uintptr_t)rows_in) & 3) == 0) {
         const unsigned nb = (unsigned)((groups + 63) / 64);     // 64 groups x 4 lanes
         const size_t lds = (((size_t)m * k + 15) & ~(size_t)15) + 64 * (size_t)k +
                            64 * (size_t)(k + 1) * 4;
+        note_kernel("decode_prep_lane_kernel");
         decode_prep_lane_kernel<<<nb, 256, lds, st>>>(
             rows_in, rows_out, status, cenc, w.coef, w.slots, w.nout, rec_rows, groups, k, m, bb,
             rmax);
@@ -1065,7 +1044,8 @@ hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t
     while (nwv > 1 && fixed + (size_t)nwv * scratch > 64 * 1024) nwv >>= 1;
     const size_t lds = fixed + (size_t)nwv * scratch;
     const long long want = (groups + nwv - 1) / nwv;
-    const unsigned nb = (unsigned)std::min<long long>(want, (long long)num_cus() * 16);
+    const unsigned nb = (unsigned)std::min<long long>(want, (long long)t.cus * 16);
+    note_kernel("decode_prep_kernel");
     decode_prep_kernel<<<nb, nwv * 64, lds, st>>>(rows_in, rows_out, status, cenc, w.coef,
                                                    w.slots, w.nout, rec_rows, groups, k, m, bb,
                                                    rc, rmax, nchunk, scratch);
@@ -1073,18 +1053,20 @@ hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t
 }
 
 hipError_t launch_gf_decode(const uint8_t* blocks, uint8_t* out, DecodeWork w, int k, int m,
-                            int bb, long long groups, int rc, int rmax, hipStream_t st) {
+                            int bb, long long groups, int rc, int rmax, hipStream_t st,
+                            const Tune& t) {
     const int nchunk = (rmax + rc - 1) / rc;
     const int rcp = rc < 4 ? 4 : rc;
     return gf_apply_dispatch<true>(blocks, out, w.coef, w.slots, w.nout, k, m, bb, groups, rc,
                                    nchunk, rmax, (long long)nchunk * k * rcp,
-                                   (long long)k * bb, st);
+                                   (long long)k * bb, st, t);
 }
 
 hipError_t launch_scatter_recovered(const uint8_t* scratch, uint8_t* out, DecodeWork w, int k,
                                    int bb, int rmax, long long groups, hipStream_t st) {
     const long long units = groups * rmax;
     if (units <= 0) return hipSuccess;
+    note_kernel("scatter_recovered_kernel");
     scatter_recovered_kernel<<<blocks_for_waves(units), 256, 0, st>>>(scratch, out, w.slots,
                                                                       w.nout, k, bb, rmax,
                                                                       units);
@@ -1093,12 +1075,12 @@ hipError_t launch_scatter_recovered(const uint8_t* scratch, uint8_t* out, Decode
 
 hipError_t launch_gf_decode_scratch(const uint8_t* blocks, uint8_t* scratch, DecodeWork w,
                                    int k, int m, int bb, long long groups, int rc, int rmax,
-                                   hipStream_t st) {
+                                   hipStream_t st, const Tune& t) {
     const int nchunk = (rmax + rc - 1) / rc;
     const int rcp = rc < 4 ? 4 : rc;
     return gf_apply_dispatch<true>(blocks, scratch, w.coef, nullptr, w.nout, k, m, bb, groups,
                                    rc, nchunk, rmax, (long long)nchunk * k * rcp,
-                                   (long long)rmax * bb, st);
+                                   (long long)rmax * bb, st, t);
 }
 
 hipError_t launch_synth_fill(uint8_t* dst, unsigned long long bytes, unsigned long long seed,

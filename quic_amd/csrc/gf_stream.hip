@@ -280,55 +280,31 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     stream_wait_vmcnt<0>();
 }
 
-namespace {
-
-int senv(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
-int stream_cus() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            n <= 0)
-            n = 256;
-    }
-    return n;
-}
-
-int stream_ring() {
-    const int r = senv("QFEC_STREAM_RING", 10);
-    return r < 4 ? 4 : (r > 36 ? 36 : r);
-}
-
-}  // namespace
-
-bool gf_stream_supported(int k, int m, int bb, int rc, bool decode) {
-    if (!senv("QFEC_STREAM", 1)) return false;
-    if (!decode && !senv("QFEC_STREAM_ENC", 1)) return false;   // 0: flat gf_apply encode
+bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& t) {
+    (void)m;
+    (void)decode;
+    if (!t.stream) return false;
     if (bb != 1352) return false;                        // S = 169 instantiated
     if (rc != 2 && rc != 4 && rc != 8) return false;
     if (((long long)k * bb) % 16 != 0) return false;     // 16-byte aligned group starts
-    (void)m;
     return true;
 }
 
 hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef,
                             const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
                             long long groups, int rc, int rmax, long long coef_gstride,
-                            long long out_gstride, bool decode, hipStream_t st) {
+                            long long out_gstride, bool decode, hipStream_t st,
+                            const Tune& t) {
     if (groups <= 0) return hipSuccess;
     if (((uintptr_t)in & 15) != 0 || ((uintptr_t)slots & 3) != 0) return hipErrorInvalidValue;
-    const int R = stream_ring();
+    const int R = t.stream_ring;
+    if (R < 4 || R > 36) return hipErrorInvalidValue;
     const size_t lds = (size_t)kStreamWaves * R * 1024;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int per_cu = (int)((160 * 1024) / lds);
     const long long want = (groups + kStreamWaves - 1) / kStreamWaves;
-    long long cap = (long long)stream_cus() * per_cu;
-    if (const int lim = senv("QFEC_STREAM_GRID", 0)) cap = lim;   // tests: many groups per wave
+    long long cap = (long long)t.cus * per_cu;
+    if (t.stream_grid > 0) cap = t.stream_grid;          // tests: many groups per wave
     const unsigned grid = (unsigned)std::min<long long>(want, cap);
     const unsigned threads = kStreamWaves * 64;
 #define QS_GO(RCV, DEC, RCPV)                                                                \
@@ -336,6 +312,7 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
                        st, in, out, coef, slots, nout, groups, k, m, rmax, coef_gstride,       \
                        out_gstride, R)
     if (bb != 1352) return hipErrorInvalidValue;
+    note_kernel(decode ? "gf_stream_kernel<decode>" : "gf_stream_kernel<encode>");
     if (decode) {
         switch (rc) {
             case 2: QS_GO(2, true, 4); break;

@@ -174,36 +174,19 @@ __global__ __launch_bounds__(256) void xor_dma_kernel(
 // ------------------------------------------------------------------------- launcher
 namespace {
 
-int xenv(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
-int xor_cus() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            n <= 0)
-            n = 256;
-    }
-    return n;
-}
-
 struct XorPlan {
-    int ndma = 0, nslot = 2, waves = 4;
+    int ndma = 0, nslot = 2, waves = 3;
     size_t lds = 0;
 };
 
-// Ring shape: QFEC_XOR_SLOTS / QFEC_XOR_WAVES override the default (2 slots x 3 waves,
-// the best of the 2-4 x 1-4 sweep in profiles/r01/A_*.txt).
-bool xor_plan(int k, int bb, XorPlan* p) {
+// Ring shape: t.xor_slots x t.xor_waves (default 2 slots x 3 waves, the best of the
+// 2-4 x 1-4 sweep in profiles/r01/A_*.txt).
+bool xor_plan(int k, int bb, const Tune& t, XorPlan* p) {
     const long long gb = (long long)k * bb;
     if (bb % 8 != 0 || gb % 16 != 0 || gb < 16) return false;
     p->ndma = (int)((gb + 1023) / 1024);
-    p->nslot = xenv("QFEC_XOR_SLOTS", 2);
-    p->waves = xenv("QFEC_XOR_WAVES", 3);
+    p->nslot = t.xor_slots;
+    p->waves = t.xor_waves;
     if (p->nslot < 2 || p->nslot > 4 || p->waves < 1 || p->waves > 4) return false;
     p->lds = (size_t)p->waves * p->nslot * (p->ndma * 1024 + 80) + (size_t)p->waves * 64;
     if (p->lds > 160 * 1024) return false;
@@ -214,15 +197,18 @@ bool xor_plan(int k, int bb, XorPlan* p) {
 template <bool DECODE, bool FUSED, bool COMPACT, int NSLOT, int N>
 hipError_t xor_go(const XorPlan& p, const uint8_t* in, uint8_t* out, const uint8_t* eidx,
                   const uint8_t* rows_in, uint8_t* rows_out, int32_t* status, int k, int bb,
-                  long long G, long long ogs, hipStream_t st) {
+                  long long G, long long ogs, hipStream_t st, int cus) {
     if constexpr (N > 20 || (NSLOT - 1) * (N + (DECODE ? 1 : 0)) > 63) {
         return hipErrorInvalidValue;
     } else {
         if (p.ndma != N)
-            return xor_go<DECODE, FUSED, COMPACT, NSLOT, N + 1>(p, in, out, eidx, rows_in, rows_out, status, k,
-                                                bb, G, ogs, st);
+            return xor_go<DECODE, FUSED, COMPACT, NSLOT, N + 1>(p, in, out, eidx, rows_in, rows_out,
+                                                                status, k, bb, G, ogs, st, cus);
         const long long want = (G + p.waves - 1) / p.waves;
-        const unsigned nb = (unsigned)std::min<long long>(want, (long long)xor_cus());
+        const unsigned nb = (unsigned)std::min<long long>(want, (long long)cus);
+        note_kernel(DECODE ? (COMPACT ? "xor_dma_kernel<decode,recovered>"
+                                      : "xor_dma_kernel<decode>")
+                           : "xor_dma_kernel<encode>");
         xor_dma_kernel<N, NSLOT, DECODE, FUSED, 0, COMPACT><<<nb, p.waves * 64, p.lds, st>>>(
             in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs);
         return hipGetLastError();
@@ -232,42 +218,42 @@ hipError_t xor_go(const XorPlan& p, const uint8_t* in, uint8_t* out, const uint8
 template <bool DECODE, bool FUSED, bool COMPACT = false>
 hipError_t xor_dispatch(const XorPlan& p, const uint8_t* in, uint8_t* out, const uint8_t* eidx,
                         const uint8_t* rows_in, uint8_t* rows_out, int32_t* status, int k,
-                        int bb, long long G, long long ogs, hipStream_t st) {
+                        int bb, long long G, long long ogs, hipStream_t st, int cus) {
     switch (p.nslot) {
-        case 2: return xor_go<DECODE, FUSED, COMPACT, 2, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st);
-        case 3: return xor_go<DECODE, FUSED, COMPACT, 3, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st);
-        case 4: return xor_go<DECODE, FUSED, COMPACT, 4, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st);
+        case 2: return xor_go<DECODE, FUSED, COMPACT, 2, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st, cus);
+        case 3: return xor_go<DECODE, FUSED, COMPACT, 3, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st, cus);
+        case 4: return xor_go<DECODE, FUSED, COMPACT, 4, 1>(p, in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs, st, cus);
         default: return hipErrorInvalidValue;
     }
 }
 
 }  // namespace
 
-bool xor_dma_ok(const void* in, const void* out, int k, int bb, long long ogs) {
-    if (xenv("QFEC_NO_DMA", 0)) return false;
+bool xor_dma_ok(const void* in, const void* out, int k, int bb, long long ogs, const Tune& t) {
+    if (!t.dma) return false;
     XorPlan p;
-    return xor_plan(k, bb, &p) && ((uintptr_t)in & 15) == 0 &&
+    return xor_plan(k, bb, t, &p) && ((uintptr_t)in & 15) == 0 &&
            (((uintptr_t)out | (uintptr_t)ogs) & 7) == 0;
 }
 
 hipError_t launch_xor_dma(const uint8_t* in, uint8_t* out, const uint8_t* eidx,
                           const uint8_t* rows_in, uint8_t* rows_out, int32_t* status, int k,
                           int bb, long long groups, long long out_gstride, bool decode,
-                          hipStream_t st, bool compact) {
+                          hipStream_t st, const Tune& t, bool compact) {
     if (groups <= 0) return hipSuccess;
     XorPlan p;
-    if (!xor_plan(k, bb, &p)) return hipErrorInvalidValue;
+    if (!xor_plan(k, bb, t, &p)) return hipErrorInvalidValue;
     if (!decode)
         return xor_dispatch<false, false>(p, in, out, eidx, rows_in, rows_out, status, k, bb,
-                                          groups, out_gstride, st);
+                                          groups, out_gstride, st, t.cus);
     if (rows_in && compact)
         return xor_dispatch<true, true, true>(p, in, out, eidx, rows_in, rows_out, status, k,
-                                              bb, groups, out_gstride, st);
+                                              bb, groups, out_gstride, st, t.cus);
     if (rows_in)
         return xor_dispatch<true, true>(p, in, out, eidx, rows_in, rows_out, status, k, bb,
-                                        groups, out_gstride, st);
+                                        groups, out_gstride, st, t.cus);
     return xor_dispatch<true, false>(p, in, out, eidx, rows_in, rows_out, status, k, bb, groups,
-                                     out_gstride, st);
+                                     out_gstride, st, t.cus);
 }
 
 }  // namespace qfec

@@ -118,6 +118,19 @@ class FecEngine:
         except Exception:
             pass
 
+    def set_option(self, name, value):
+        """Launch-shape option of this engine's context (qfec_ctx_set_option)."""
+        rc = self.lib.qfec_ctx_set_option(self._h, name.encode(), int(value))
+        if rc:
+            raise FecError(rc, f"qfec_ctx_set_option({name})")
+
+    def get_option(self, name):
+        v = ctypes.c_int()
+        rc = self.lib.qfec_ctx_get_option(self._h, name.encode(), ctypes.byref(v))
+        if rc:
+            raise FecError(rc, f"qfec_ctx_get_option({name})")
+        return v.value
+
     def reserve(self, k, m, block_bytes, groups):
         rc = self.lib.qfec_reserve(self._h, k, m, block_bytes, groups)
         if rc:
@@ -185,6 +198,12 @@ class FecEngine:
         if rc:
             raise FecError(rc, "qfec_decode_batch_host")
         return blocks, rows, status
+
+
+def last_kernels():
+    """Kernels the calling thread's last engine call launched (qfec_last_kernels)."""
+    v = load().qfec_last_kernels()
+    return v.decode() if v else ""
 
 
 def _hptr(t):

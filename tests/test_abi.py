@@ -77,3 +77,11 @@ def test_cauchy_matrix_rejects_bad_params():
 def test_init_version_mismatch_is_minus_one():
     # version check happens before any device access (cauchy_256.cpp:389-398)
     assert fec._cauchy_256_init(1) == -1
+
+
+def test_no_environment_knobs_in_product():
+    """Launch shapes are per-context options (qfec_ctx_set_option); the only environment
+    variable the library reads is QFEC_DEVICE (device of the drop-ins' default context)."""
+    out = subprocess.run(["strings", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    names = set(re.findall(r"\bQFEC_[A-Z0-9_]+", out))
+    assert names <= {"QFEC_DEVICE"}, names

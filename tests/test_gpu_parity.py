@@ -338,16 +338,25 @@ def test_decode_recovered_host(engine, oracle):
 
 
 # ------------------------------------------- gf_stream ring (many groups per wave)
+@pytest.fixture
+def tuned_engine():
+    """A fresh engine (own context) for tests that change launch options."""
+    from quic_amd.fec import FecEngine
+    eng = FecEngine(0)
+    yield eng
+    eng.close()
+
+
 @pytest.mark.parametrize("ring", [4, 7, 10])
 @pytest.mark.parametrize("k,m,r", [(32, 4, 2), (32, 3, 3), (250, 5, 5), (32, 8, 6)])
-def test_stream_ring_many_groups_per_wave(engine, oracle, monkeypatch, ring, k, m, r):
+def test_stream_ring_many_groups_per_wave(tuned_engine, oracle, ring, k, m, r):
     """One workgroup (4 waves) walks every group, so each wave streams several groups
     through its LDS ring back to back (the ring wraps inside blocks and across groups);
     every third group has no loss (decode skips it but its pieces stay in the stream)."""
     import torch
-    monkeypatch.setenv("QFEC_STREAM_GRID", "1")
-    monkeypatch.setenv("QFEC_STREAM_RING", str(ring))
-    monkeypatch.setenv("QFEC_STREAM_ENC", "1")
+    engine = tuned_engine
+    engine.set_option("stream_grid", 1)
+    engine.set_option("stream_ring", ring)
     bb, G = 1352, 23
     data = synth.group_data(900 + k + m + ring, k, bb, G)
     p_or, rc_or = oracle.encode_batch(k, m, bb, data)
@@ -375,3 +384,187 @@ def test_stream_ring_many_groups_per_wave(engine, oracle, monkeypatch, ring, k, 
     got = host(rec)
     mask = exp_rows != 255
     np.testing.assert_array_equal(got[mask], exp[mask])
+
+
+# ------------------------------------------------- non-default launch options
+OPTION_SETS = [
+    {"xor_slots": 3, "xor_waves": 3}, {"xor_slots": 4, "xor_waves": 2}, {"xor_waves": 1},
+    {"dma": 0}, {"stream": 0}, {"stream": 0, "pd": 1}, {"stream": 0, "pd": 3},
+    {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
+    {"stream_ring": 36}, {"host_chunk_mb": 1},
+]
+
+
+@pytest.mark.parametrize("opts", OPTION_SETS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+def test_options_parity(tuned_engine, oracle, opts):
+    """Every launch option the library accepts produces the oracle's bytes."""
+    engine = tuned_engine
+    for name, v in opts.items():
+        engine.set_option(name, v)
+        assert engine.get_option(name) == v
+    for (k, m, bb, r) in [(10, 1, 1352, 1), (32, 4, 1352, 2), (16, 8, 9008, 5), (17, 6, 136, 6)]:
+        G = 7
+        data = synth.group_data(555 + k + m, k, bb, G)
+        p_or, rc_or = oracle.encode_batch(k, m, bb, data)
+        p_gpu, rc = gpu_encode(engine, k, m, bb, data)
+        assert rc == rc_or
+        np.testing.assert_array_equal(p_gpu, p_or)
+        rows, src = synth.loss_patterns(k, m, r, G, 99 + k, shuffle=True)
+        recv = synth.assemble_received(data, p_or, src)
+        b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+        b, rr, s = gpu_decode(engine, k, m, bb, recv, rows, inplace=True)
+        np.testing.assert_array_equal(s, s_or)
+        np.testing.assert_array_equal(rr, r_or)
+        np.testing.assert_array_equal(b, b_or)
+        if "host_chunk_mb" in opts:
+            b2, rr2, s2 = engine.decode_host(k, m, bb, recv, rows)
+            np.testing.assert_array_equal(b2, b_or)
+
+
+def test_option_errors(tuned_engine):
+    with pytest.raises(fec.FecError):
+        tuned_engine.set_option("no_such_option", 1)
+    with pytest.raises(fec.FecError):
+        tuned_engine.set_option("enc_rc", 3)
+    with pytest.raises(fec.FecError):
+        tuned_engine.set_option("stream_ring", 99)
+    assert tuned_engine.get_option("cus") > 0
+
+
+def test_last_kernels_reports_launches(tuned_engine):
+    """The library names the kernels it launched (bench.py reports these)."""
+    import torch
+    engine = tuned_engine
+    for (k, m, bb, enc, dec) in [
+            (10, 1, 1352, "xor_dma_kernel<encode>", "xor_dma_kernel<decode,recovered>"),
+            (32, 4, 1352, "gf_stream_kernel<encode>", "gf_stream_kernel<decode>")]:
+        G = 8
+        data = torch.from_numpy(synth.group_data(3, k, bb, G)).cuda()
+        parity = torch.zeros((G, m, bb), dtype=torch.uint8, device="cuda")
+        engine.encode(k, m, bb, data, parity)
+        assert fec.last_kernels() == enc
+        rows, src = synth.loss_patterns(k, m, min(k, m), G, 5)
+        rmax = min(k, m)
+        rec = torch.zeros((G, rmax, bb), dtype=torch.uint8, device="cuda")
+        rr = torch.zeros((G, rmax), dtype=torch.uint8, device="cuda")
+        engine.decode_recovered(k, m, bb, data, dev(rows), rec, rr)
+        assert fec.last_kernels().endswith(dec)
+    engine.set_option("stream", 0)
+    data = torch.zeros((4, 32, 1352), dtype=torch.uint8, device="cuda")
+    parity = torch.zeros((4, 4, 1352), dtype=torch.uint8, device="cuda")
+    engine.encode(32, 4, 1352, data, parity)
+    assert fec.last_kernels().startswith("gf_apply_kernel<encode")
+    torch.cuda.synchronize()
+
+
+# ------------------------------------------------- concurrency: streams and contexts
+def _case(k, m, bb, r, G, seed):
+    data = synth.group_data(seed, k, bb, G)
+    rows, src = synth.loss_patterns(k, m, r, G, seed + 1, shuffle=True)
+    return data, rows, src
+
+
+def test_two_contexts_two_streams(oracle):
+    """Two contexts on device 0, each on its own stream, running A- and B-shaped batches
+    at the same time; both bit-exact vs the oracle (contexts share no state)."""
+    import torch
+    from quic_amd.fec import FecEngine
+    e1, e2 = FecEngine(0), FecEngine(0)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    cases = [(e1, s1, (10, 1, 1352, 1, 512, 71)), (e2, s2, (32, 4, 1352, 2, 256, 72))]
+    outs = []
+    for eng, st, (k, m, bb, r, G, seed) in cases:
+        data, rows, src = _case(k, m, bb, r, G, seed)
+        with torch.cuda.stream(st):
+            d = dev(data)
+            p = torch.zeros((G, m, bb), dtype=torch.uint8, device="cuda")
+            rec = torch.zeros((G, min(k, m), bb), dtype=torch.uint8, device="cuda")
+            rr = torch.zeros((G, min(k, m)), dtype=torch.uint8, device="cuda")
+            b = torch.empty((G, k, bb), dtype=torch.uint8, device="cuda")
+            sd = dev(src)
+            rw = dev(rows)
+        outs.append((eng, st, k, m, bb, r, G, data, rows, src, d, p, rec, rr, b, sd, rw))
+    torch.cuda.synchronize()
+    for _ in range(3):   # interleave the enqueues of the two contexts
+        for (eng, st, k, m, bb, r, G, data, rows, src, d, p, rec, rr, b, sd, rw) in outs:
+            with torch.cuda.stream(st):
+                assert eng.encode(k, m, bb, d, p, stream=st.cuda_stream) == 0
+                fec.synth_gather(d, p, sd, b, k, m, bb, stream=st.cuda_stream)
+                eng.decode_recovered(k, m, bb, b, rw, rec, rr, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    for (eng, st, k, m, bb, r, G, data, rows, src, d, p, rec, rr, b, sd, rw) in outs:
+        p_or, _ = oracle.encode_batch(k, m, bb, data)
+        np.testing.assert_array_equal(host(p), p_or)
+        recv = synth.assemble_received(data, p_or, src)
+        b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+        exp, exp_rows = expected_recovered(k, m, bb, rows, b_or, r_or, s_or)
+        np.testing.assert_array_equal(host(rr), exp_rows)
+        mask = exp_rows != 255
+        np.testing.assert_array_equal(host(rec)[mask], exp[mask])
+    e1.close()
+    e2.close()
+
+
+def test_one_context_two_streams_decode(tuned_engine, oracle):
+    """Two decodes of one context enqueued on two streams back to back share the decode
+    workspace; the library orders the second behind the first, so both are exact."""
+    import torch
+    engine = tuned_engine
+    k, m, bb = 32, 4, 1352
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    runs = []
+    for i, (r, G) in enumerate([(4, 4096), (1, 4096)]):
+        data, rows, src = _case(k, m, bb, r, G, 300 + i)
+        p_or, _ = oracle.encode_batch(k, m, bb, data)
+        recv = synth.assemble_received(data, p_or, src)
+        rec = torch.zeros((G, 4, bb), dtype=torch.uint8, device="cuda")
+        rr = torch.zeros((G, 4), dtype=torch.uint8, device="cuda")
+        runs.append((recv, rows, dev(recv), dev(rows), rec, rr))
+    torch.cuda.synchronize()
+    for (recv, rows, b, rw, rec, rr), st in zip(runs, (s1, s2)):
+        engine.decode_recovered(k, m, bb, b, rw, rec, rr, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    for (recv, rows, b, rw, rec, rr) in runs:
+        b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+        exp, exp_rows = expected_recovered(k, m, bb, rows, b_or, r_or, s_or)
+        np.testing.assert_array_equal(host(rr), exp_rows)
+        mask = exp_rows != 255
+        np.testing.assert_array_equal(host(rec)[mask], exp[mask])
+
+
+# ------------------------------------------------- config C: one GPU's shard
+def test_config_c_shard_round_trip(engine, oracle):
+    """BASELINE.json configs[3]: 1,048,576 groups of (32 + 4) x 1350 B split over 8 GPUs;
+    one GPU's shard is 131,072 groups (rank 3's range of the global stream here).  Encode,
+    lose 2 data blocks per group, decode in the recovered-blocks layout: every recovered
+    block equals its original; sampled groups match the oracle byte for byte."""
+    import torch
+    from quic_amd import shard
+    k, m, bb, r = 32, 4, 1352, 2
+    g0, G = shard.strong_range(1048576, 8, 3)
+    assert G == 131072
+    data = torch.empty((G, k, bb), dtype=torch.uint8, device="cuda")
+    fec.synth_fill(data, seed=77, byte_offset=shard.data_byte_offset(g0, k, bb))
+    parity = torch.zeros((G, m, bb), dtype=torch.uint8, device="cuda")
+    assert engine.encode(k, m, bb, data, parity) == 0
+    rows, src = synth.loss_patterns(k, m, r, G, shard.loss_seed(77, 3))
+    blocks = torch.empty((G, k, bb), dtype=torch.uint8, device="cuda")
+    fec.synth_gather(data, parity, dev(src), blocks, k, m, bb)
+    rec = torch.zeros((G, 4, bb), dtype=torch.uint8, device="cuda")
+    rr = torch.zeros((G, 4), dtype=torch.uint8, device="cuda")
+    st = torch.full((G,), 9, dtype=torch.int32, device="cuda")
+    engine.decode_recovered(k, m, bb, blocks, dev(rows), rec, rr, status=st)
+    torch.cuda.synchronize()
+    assert int(st.abs().max()) == 0
+    got = rr != 255
+    assert bool((got.sum(dim=1) == r).all())
+    g_idx = torch.arange(G, device="cuda")[:, None].expand(G, 4)[got]
+    assert torch.equal(rec[got], data[g_idx, rr.long()[got]])
+    # the shard is the global stream at its offset
+    np.testing.assert_array_equal(host(data[1]).ravel(),
+                                  synth.stream_bytes(77, (g0 + 1) * k * bb, k * bb))
+    sample = [0, 4097, G - 1]
+    p_or, _ = oracle.encode_batch(k, m, bb, host(data[sample]))
+    np.testing.assert_array_equal(host(parity[sample]), p_or)
+    del data, parity, blocks, rec
+    torch.cuda.empty_cache()
