@@ -489,6 +489,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"xor_slots", &t.xor_slots, 2, 4},     {"xor_waves", &t.xor_waves, 1, 4},
         {"dma", &t.dma, 0, 1},                 {"stream", &t.stream, 0, 1},
         {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
+        {"const_enc", &t.const_enc, 0, 1},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -510,6 +511,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
     const std::pair<const char*, int> opts[] = {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
+        {"const_enc", t.const_enc},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb},
     };

@@ -23,6 +23,7 @@ struct Tune {
     int stream = 1;           // m > 1, small blocks: gf_stream (0: gf_apply)
     int stream_ring = 10;     // gf_stream: 1 KiB ring slots per wave (4..36)
     int stream_grid = 0;      // gf_stream: grid cap in workgroups (0: CUs x per-CU fit)
+    int const_enc = 1;        // encode kernels specialised for fixed (k, m) where compiled
     int pd = 2;               // gf_apply: register pipeline depth (1..3)
     int flat = 1;             // gf_apply: lane-flat encode
     int enc_rc = 8;           // gf_apply: encode outputs per wave (2, 4, 8)

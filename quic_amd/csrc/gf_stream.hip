@@ -31,10 +31,24 @@
 // Decode: per-group coefficients from decode_prep_kernel ([G][1][k][RCP]), outputs go to
 // slots[g][j] (or j, recovered-blocks layout) and groups with nout == 0 are skipped.  All of
 // a group's blocks are in LDS before any of its stores, so in place is safe.
+#include <utility>
+
+#include "cauchy_const.h"
 #include "fec_kernels.h"
 #include "gf_bitslice.h"
 
 namespace qfec {
+
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): a loop whose index is
+// a compile-time constant in every iteration (the encode coefficients of a fixed (k, m)).
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 #define QS_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define QS_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
@@ -74,7 +88,11 @@ constexpr int kStreamWaves = 4;            // waves per workgroup (independent)
 // RCPT = byte stride of a coefficient row in the table (max(4, table rc)).  Encode is
 // instantiated with RC = m exactly, so the per-output `j < n` test folds away (at run time
 // the compiler turned it into a lane mask: 2 VALU + 2 SALU per output and block).
-template <int RC, int S, bool DECODE, int RCPT = (RC < 4 ? 4 : RC)>
+// KC > 0 (encode only): the code is fixed, k = KC and m = RC <= 6, and the coefficients come
+// from cauchy_const.h at compile time.  The block loop is then fully unrolled and every
+// 8x8 bit expansion folds into its straight-line XORs: no coefficient loads and no scalar
+// nibble dispatch (about 9 scalar instructions per nibble in the run-time form).
+template <int RC, int S, bool DECODE, int RCPT = (RC < 4 ? 4 : RC), int KC = 0>
 __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
@@ -96,6 +114,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const long long g0 = (long long)blockIdx.x * kStreamWaves + w;
     if (g0 >= groups) return;
     const long long cnt = (groups - 1 - g0) / W + 1;   // groups of this wave
+    static_assert(KC == 0 || (!DECODE && RC >= 2 && RC <= 6), "compile-time codes: encode, m <= 6");
+    if constexpr (KC > 0) k = KC;
     const int gb = k * BB;
     const int NP = (gb + 1023) >> 10;                  // pieces per group
     const int c = lane < NW ? lane : NW - 1;           // idle lanes shadow the last word
@@ -154,8 +174,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     // time.  No mirror of the first slots is kept, so all R * 1 KiB of the wave's LDS are
     // ring slots (R = 10 at 16 waves per CU, against 8 slots + 2 KiB mirror before).
     auto read_block = [&](uint32_t bp, uint32_t (&lo)[8], uint32_t (&hi)[8]) {
+        // the lane's byte offset, opaque to the optimiser: in the fully unrolled (KC > 0)
+        // form it would otherwise precompute every block's addresses up front
+        uint32_t c4 = 4u * (uint32_t)c;
+        if constexpr (KC > 0) asm volatile("" : "+v"(c4));
         if (bp + (uint32_t)BB + 4u <= (uint32_t)RB) {
-            const uint8_t* L = ring + bp + 4u * (uint32_t)c;
+            const uint8_t* L = ring + bp + c4;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
                 const int o = t * S;
@@ -164,7 +188,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                 hi[t] = (o & 3) ? q[1] : 0u;
             }
         } else {
-            const uint32_t base = bp + 4u * (uint32_t)c;
+            const uint32_t base = bp + c4;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
                 const int o = t * S;
@@ -209,8 +233,10 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
             fill(gbase);
             wait_block(bpos);
             read_block(bpos, lo0, hi0);
-            auto step = [&](int x, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
+            // xc: the block index, an int or (KC > 0) an integral_constant
+            auto step = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
                             uint32_t (&nhi)[8]) {
+                const int x = xc;
                 const uint32_t bn = next_pos(bpos);
                 if (x + 1 < k) {
                     fill(gbase + ((x * BB) >> 10));
@@ -225,9 +251,23 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     v.W[t] = (o & 3) ? __builtin_amdgcn_alignbyte(hi[t], lo[t], o & 3) : lo[t];
                 }
                 uint32_t cwv[NCW];
+                if constexpr (KC == 0) {
 #pragma unroll
-                for (int q = 0; q < NCW; ++q) cwv[q] = cw[x * NCW + q];
+                    for (int q = 0; q < NCW; ++q) cwv[q] = cw[x * NCW + q];
+                }
                 expand_wz(v);
+                if constexpr (KC > 0) {
+                    // row 0 is P0 (all ones); rows 1..m-1 with their compile-time coefficient
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) acc[0][r] ^= v.W[r];
+                    static_for<RC - 1>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value + 1;
+                        constexpr uint32_t cf = cauchy_coef_small(RC, j, decltype(xc)::value);
+                        apply_nibble<0>(acc[j], cf & 15u, v);
+                        apply_nibble<4>(acc[j], cf >> 4, v);
+                    });
+                    return;
+                }
 #pragma unroll
                 for (int j = 0; j < RC; ++j) {
                     if (!DECODE && j == 0) {
@@ -242,10 +282,26 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     }
                 }
             };
+            if constexpr (KC > 0) {
+                static_for<KC>([&](auto xc) {
+                    // keep each block's work in its own region: unscheduled, the compiler
+                    // hoists every LDS read of the group and needs ~490 VGPRs
+                    // and make the accumulators opaque at every block boundary: with all
+                    // coefficients constant, the XOR reassociation otherwise flattens the
+                    // 32 blocks' sums into one tree and keeps every block's W/Z live
+#pragma unroll
+                    for (int j = 0; j < RC; ++j)
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
+                    if constexpr (decltype(xc)::value % 2 == 0) step(xc, lo0, hi0, lo1, hi1);
+                    else step(xc, lo1, hi1, lo0, hi0);
+                });
+            } else {
 #pragma unroll 1
-            for (int x = 0; x < k; x += 2) {
-                step(x, lo0, hi0, lo1, hi1);
-                if (x + 1 < k) step(x + 1, lo1, hi1, lo0, hi0);
+                for (int x = 0; x < k; x += 2) {
+                    step(x, lo0, hi0, lo1, hi1);
+                    if (x + 1 < k) step(x + 1, lo1, hi1, lo0, hi0);
+                }
             }
             // ---- outputs: fixed instruction count per output (dropped lanes, no branches)
 #pragma unroll
@@ -312,8 +368,8 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
                        st, in, out, coef, slots, nout, groups, k, m, rmax, coef_gstride,       \
                        out_gstride, R)
     if (bb != 1352) return hipErrorInvalidValue;
-    note_kernel(decode ? "gf_stream_kernel<decode>" : "gf_stream_kernel<encode>");
     if (decode) {
+        note_kernel("gf_stream_kernel<decode>");
         switch (rc) {
             case 2: QS_GO(2, true, 4); break;
             case 4: QS_GO(4, true, 4); break;
@@ -323,6 +379,15 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     } else {
         // one output per register set: RC = m; the table row stride is max(4, rc)
         if ((rc < 4 ? 4 : rc) != (m <= 4 ? 4 : 8)) return hipErrorInvalidValue;
+        if (t.const_enc && k == 32 && m == 4) {
+            // BASELINE configs B/C: the code is fixed at compile time
+            note_kernel("gf_stream_kernel<encode,k32m4>");
+            hipLaunchKernelGGL((gf_stream_kernel<4, 169, false, 4, 32>), dim3(grid), dim3(threads),
+                               lds, st, in, out, coef, slots, nout, groups, k, m, rmax,
+                               coef_gstride, out_gstride, R);
+            return hipGetLastError();
+        }
+        note_kernel("gf_stream_kernel<encode>");
         switch (m) {
             case 2: QS_GO(2, false, 4); break;
             case 3: QS_GO(3, false, 4); break;

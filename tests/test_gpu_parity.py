@@ -391,7 +391,7 @@ OPTION_SETS = [
     {"xor_slots": 3, "xor_waves": 3}, {"xor_slots": 4, "xor_waves": 2}, {"xor_waves": 1},
     {"dma": 0}, {"stream": 0}, {"stream": 0, "pd": 1}, {"stream": 0, "pd": 3},
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
-    {"stream_ring": 36}, {"host_chunk_mb": 1},
+    {"stream_ring": 36}, {"host_chunk_mb": 1}, {"const_enc": 0},
 ]
 
 
@@ -437,7 +437,8 @@ def test_last_kernels_reports_launches(tuned_engine):
     engine = tuned_engine
     for (k, m, bb, enc, dec) in [
             (10, 1, 1352, "xor_dma_kernel<encode>", "xor_dma_kernel<decode,recovered>"),
-            (32, 4, 1352, "gf_stream_kernel<encode>", "gf_stream_kernel<decode>")]:
+            (32, 4, 1352, "gf_stream_kernel<encode,k32m4>", "gf_stream_kernel<decode>"),
+            (32, 3, 1352, "gf_stream_kernel<encode>", "gf_stream_kernel<decode>")]:
         G = 8
         data = torch.from_numpy(synth.group_data(3, k, bb, G)).cuda()
         parity = torch.zeros((G, m, bb), dtype=torch.uint8, device="cuda")

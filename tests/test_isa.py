@@ -23,8 +23,11 @@ def stream_isa(tmp_path_factory):
         pytest.skip("hipcc not available")
     out = tmp_path_factory.mktemp("isa") / "gf_stream.s"
     src = os.path.join(ROOT, "quic_amd", "csrc", "gf_stream.hip")
+    subprocess.run(["python3", os.path.join(ROOT, "tools", "gen_cauchy_const.py")], check=True,
+                   capture_output=True)
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17",
                     "-mllvm", "-structurizecfg-skip-uniform-regions=true", "-DQFEC_BUILD",
+                    "-I", os.path.join(ROOT, "build", "gen"),
                     "--cuda-device-only", "-S", "-o", str(out), src],
                    check=True, capture_output=True)
     text = out.read_text()
