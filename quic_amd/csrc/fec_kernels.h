@@ -21,7 +21,7 @@ struct Tune {
     int xor_waves = 3;        //                 waves per workgroup (1..4)
     int dma = 1;              // m = 1: LDS-DMA ring kernel (0: flat register kernel)
     int stream = 1;           // m > 1, small blocks: gf_stream (0: gf_apply)
-    int stream_ring = 10;     // gf_stream: 1 KiB ring slots per wave (4..36)
+    int stream_ring = 8;      // gf_stream: 1 KiB ring slots per wave (4..36), + 2 mirrored
     int stream_grid = 0;      // gf_stream: grid cap in workgroups (0: CUs x per-CU fit)
     int const_enc = 1;        // encode kernels specialised for fixed (k, m) where compiled
     int pd = 2;               // gf_apply: register pipeline depth (1..3)

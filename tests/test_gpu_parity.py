@@ -569,3 +569,39 @@ def test_config_c_shard_round_trip(engine, oracle):
     np.testing.assert_array_equal(host(parity[sample]), p_or)
     del data, parity, blocks, rec
     torch.cuda.empty_cache()
+
+
+# ------------------------------------------------- gf_stream at other block sizes
+@pytest.mark.parametrize("bb", [1344, 1000, 520, 136, 2048, 8, 1352])
+@pytest.mark.parametrize("k,m,r", [(32, 4, 2), (10, 3, 3), (6, 8, 5)])
+def test_stream_any_small_block(engine, oracle, bb, k, m, r):
+    """Groups whose padded blocks are at most 2 KiB (quic_fec_group.cc:344-352 pads to the
+    group's longest packet) run the streaming kernel, not gf_apply; bit-exact vs the
+    oracle, encode and both decode layouts."""
+    import torch
+    if (k * bb) % 16:
+        pytest.skip("odd k with bb % 16 == 8: groups not 16-byte aligned (gf_apply path)")
+    G = 9
+    data = synth.group_data(bb + 17 * k + m, k, bb, G)
+    p_or, rc_or = oracle.encode_batch(k, m, bb, data)
+    p_gpu, rc = gpu_encode(engine, k, m, bb, data)
+    assert fec.last_kernels().startswith("gf_stream_kernel<encode")
+    assert rc == rc_or == 0
+    np.testing.assert_array_equal(p_gpu, p_or)
+    rows, src = synth.loss_patterns(k, m, r, G, 3 + bb, shuffle=True)
+    recv = synth.assemble_received(data, p_or, src)
+    b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+    b, rr, s = gpu_decode(engine, k, m, bb, recv, rows, inplace=True)
+    assert "gf_stream_kernel<decode" in fec.last_kernels()
+    np.testing.assert_array_equal(s, s_or)
+    np.testing.assert_array_equal(rr, r_or)
+    np.testing.assert_array_equal(b, b_or)
+    exp, exp_rows = expected_recovered(k, m, bb, rows, b_or, r_or, s_or)
+    rmax = min(k, m)
+    rec = torch.zeros((G, rmax, bb), dtype=torch.uint8, device="cuda")
+    rec_rows = torch.zeros((G, rmax), dtype=torch.uint8, device="cuda")
+    engine.decode_recovered(k, m, bb, dev(recv), dev(rows), rec, rec_rows)
+    assert "gf_stream_kernel<decode" in fec.last_kernels()
+    np.testing.assert_array_equal(host(rec_rows), exp_rows)
+    mask = exp_rows != 255
+    np.testing.assert_array_equal(host(rec)[mask], exp[mask])
