@@ -266,6 +266,11 @@ int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
                                       (long long)m * bb, false, st, c->tune));
         return 0;
     }
+    if (qfec::gf_tile_supported(k, m, bb, rc, false, c->tune) && ((uintptr_t)d_data & 15) == 0) {
+        QF_HIP(qfec::launch_gf_tile(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc, 0, 0,
+                                    (long long)m * bb, false, st, c->tune));
+        return 0;
+    }
     QF_HIP(qfec::launch_gf_encode(d_data, d_par, tab, k, m, bb, G, rc, st, c->tune));
     return 0;
 }
@@ -301,6 +306,14 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
         QF_HIP(qfec::launch_gf_stream(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
                                       rmax, (long long)nchunk * k * rcp, (long long)k * bb, true,
                                       st, c->tune));
+        return 0;
+    }
+    if (qfec::gf_tile_supported(k, m, bb, rc, true, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
+        // a group's stores follow all of its reads: in place needs no scratch
+        const int rcp = std::max(rc, 4);
+        QF_HIP(qfec::launch_gf_tile(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
+                                    rmax, (long long)nchunk * k * rcp, (long long)k * bb, true,
+                                    st, c->tune));
         return 0;
     }
     if (nchunk > 1 && d_out == d_blocks) {
@@ -363,6 +376,14 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
         QF_HIP(qfec::launch_gf_stream(d_blocks, d_rec, w.coef, nullptr, w.nout, k, m, bb, G, rc,
                                       rmax, (long long)k * rcp, (long long)rmax * bb, true, st,
                                       c->tune));
+        return 0;
+    }
+    if (qfec::gf_tile_supported(k, m, bb, rc, true, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
+        const int rcp = std::max(rc, 4);
+        const int nchunk = (rmax + rc - 1) / rc;
+        QF_HIP(qfec::launch_gf_tile(d_blocks, d_rec, w.coef, nullptr, w.nout, k, m, bb, G, rc,
+                                    rmax, (long long)nchunk * k * rcp, (long long)rmax * bb,
+                                    true, st, c->tune));
         return 0;
     }
     QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, d_rec, w, k, m, bb, G, rc, rmax, st,
@@ -489,7 +510,8 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"xor_slots", &t.xor_slots, 2, 4},     {"xor_waves", &t.xor_waves, 1, 4},
         {"dma", &t.dma, 0, 1},                 {"stream", &t.stream, 0, 1},
         {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
-        {"const_enc", &t.const_enc, 0, 1},
+        {"const_enc", &t.const_enc, 0, 1},     {"tile", &t.tile, 0, 1},
+        {"tile_grid", &t.tile_grid, 0, 1 << 20},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -511,7 +533,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
     const std::pair<const char*, int> opts[] = {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
-        {"const_enc", t.const_enc},
+        {"const_enc", t.const_enc}, {"tile", t.tile}, {"tile_grid", t.tile_grid},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb},
     };

@@ -24,6 +24,8 @@ struct Tune {
     int stream_ring = 8;      // gf_stream: 1 KiB ring slots per wave (4..36), + 2 mirrored
     int stream_grid = 0;      // gf_stream: grid cap in workgroups (0: CUs x per-CU fit)
     int const_enc = 1;        // encode kernels specialised for fixed (k, m) where compiled
+    int tile = 1;             // m > 1, 9008-byte blocks: gf_tile (0: gf_apply)
+    int tile_grid = 0;        // gf_tile: grid cap in workgroups (0: CUs x per-CU fit)
     int pd = 2;               // gf_apply: register pipeline depth (1..3)
     int flat = 1;             // gf_apply: lane-flat encode
     int enc_rc = 8;           // gf_apply: encode outputs per wave (2, 4, 8)
@@ -113,6 +115,13 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
                             long long out_gstride, bool decode, hipStream_t st,
                             const Tune& t);
 
+
+// Workgroup-shared LDS block stream for 9008-byte blocks, column-tile waves (gf_tile.hip).
+bool gf_tile_supported(int k, int m, int bb, int rc, bool decode, const Tune& t);
+hipError_t launch_gf_tile(const uint8_t* in, uint8_t* out, const uint8_t* coef,
+                          const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
+                          long long groups, int rc, int rmax, long long coef_gstride,
+                          long long out_gstride, bool decode, hipStream_t st, const Tune& t);
 
 // Synthetic workload helpers (bench / tests): splitmix64 stream and receive-set gather.
 hipError_t launch_synth_fill(uint8_t* dst, unsigned long long bytes, unsigned long long seed,

@@ -7,7 +7,20 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 namespace qfec {
+
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): a loop whose index is
+// a compile-time constant in every iteration (the encode coefficients of a fixed (k, m)).
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // v_bitop3_b32 ... bitop3:0x96

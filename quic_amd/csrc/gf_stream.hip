@@ -31,24 +31,11 @@
 // Decode: per-group coefficients from the decode prep ([G][1][k][RCP]), outputs go to
 // slots[g][j] (or j, recovered-blocks layout) and groups with nout == 0 are skipped.  All of
 // a group's blocks are in LDS before any of its stores, so in place is safe.
-#include <utility>
-
 #include "cauchy_const.h"
 #include "fec_kernels.h"
 #include "gf_bitslice.h"
 
 namespace qfec {
-
-// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): a loop whose index is
-// a compile-time constant in every iteration (the encode coefficients of a fixed (k, m)).
-template <class F, int... I>
-__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
 
 #define QS_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define QS_LPTR(p) ((__attribute__((address_space(3))) void*)(p))

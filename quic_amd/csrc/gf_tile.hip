@@ -1,0 +1,358 @@
+// gf_tile.hip — m > 1 encode / decode for jumbo blocks: BASELINE config D,
+// (128 data + 16 parity) x 9008 B blocks (9000 B payloads, quic_fec_group.cc:344-352).
+//
+// Same bit-sliced Cauchy arithmetic as gf_stream / gf_apply (cauchy_256.cpp:90-125,
+// :1419-1601, W/Z nibble expansion of gf_bitslice.h).  What differs is the shape:
+//
+// * A sub-row is s = 1126 bytes = 282 column words, so one group spans NT = 5 column tiles
+//   of 64 words, and 16 outputs need two chunks of 8 accumulators (8 outputs x 8 sub-rows
+//   = 64 VGPRs).  A workgroup is NT x NCH waves (tile, chunk) that process ONE group at a
+//   time, block by block, out of a shared LDS stream: the NPB = 9 one-KiB pieces of every
+//   block are DMA'd (global_load_lds_dwordx4, nt) into one of D + 1 block buffers, spread
+//   over the waves (each wave issues PPW pieces per block; where the pieces do not divide,
+//   the last one is loaded twice into the same LDS bytes).  D blocks are in flight; a
+//   wave waits with a counted `s_waitcnt vmcnt` for its own pieces of the next block, then
+//   one s_barrier tells it every wave's pieces landed.  Each block is read from HBM once
+//   (16-byte aligned pieces: bb % 16 == 0), its sub-rows are realigned in LDS (v_alignbyte),
+//   and the waves of one workgroup stay within one block of each other, which keeps the
+//   large unrolled encode program inside the instruction cache.
+// * Encode with a compiled code (KC, MC > 0: (128, 16)): the coefficients are compile-time
+//   constants (cauchy_const.h, cauchy_256.cpp:422-480), the block loop is unrolled and every
+//   8x8 expansion folds into straight-line XORs, with no scalar nibble dispatch — about half
+//   the instructions of the run-time form, which is issue-bound on this shape.
+// * Decode: run-time coefficients (decode prep output [G][nchunk][k][RCP]) through the
+//   scalar nibble dispatch of gf_bitslice.h.
+//
+// vmcnt bookkeeping: per block a wave issues exactly PPW DMA instructions; per group it
+// issues exactly RC * 8 * SPR stores (lanes of unused outputs dropped), so the count of
+// VMEM instructions younger than the pieces of block b + 1 is (D - 1) * PPW, plus the
+// group's stores for the first D - 1 blocks of a group (capped at 63: a smaller count only
+// waits longer).  tests/test_isa.py checks that the compiler adds no VMEM instruction or
+// vmcnt wait of its own.
+#include "cauchy_const.h"
+#include "fec_kernels.h"
+#include "gf_bitslice.h"
+
+namespace qfec {
+
+#define QT_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define QT_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+template <int N>
+__device__ __forceinline__ void tile_wait_vmcnt() {
+    static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits on gfx9");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// s_barrier with a compiler memory fence only (__syncthreads would also drain vmcnt,
+// i.e. the whole DMA pipeline)
+__device__ __forceinline__ void tile_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+__device__ __forceinline__ int tile_sload_u8(const uint8_t* __restrict__ base, long long i) {
+    const uint32_t wv = ((const uint32_t*)base)[i >> 2];
+    return (int)((wv >> (8 * (i & 3))) & 0xFFu);
+}
+
+constexpr unsigned kTDrop = 0x80000000u;   // buffer offset past any range: lane dropped
+
+template <int S>
+struct TileShape {
+    static constexpr int BB = 8 * S;
+    static constexpr int NW = (S + 3) / 4;          // column words per sub-row
+    static constexpr int NWF = S / 4;               // full words
+    static constexpr int NT = (NW + 63) / 64;       // column tiles (waves per chunk)
+    static constexpr int NPB = (BB + 1023) / 1024;  // DMA pieces per block
+    static constexpr int BBP = NPB * 1024;          // LDS bytes per block buffer
+    static constexpr int SPR = 1 + ((S >> 1) & 1) + (S & 1);   // stores per sub-row
+};
+
+// S: sub-row bytes (compile time).  RC: outputs per chunk wave, NCH chunks.  D: blocks in
+// flight (D + 2 LDS buffers).  KC, MC > 0: encode of the compiled code (k, m) = (KC, MC).
+template <int S, int RC, int NCH, bool DECODE, int D, int KC = 0, int MC = 0>
+__global__ __launch_bounds__(TileShape<S>::NT * NCH * 64, 3) void gf_tile_kernel(
+    const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
+    const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
+    int k, int m, int rmax, long long coef_gstride, long long out_gstride) {
+    using T = TileShape<S>;
+    constexpr int BB = T::BB, NW = T::NW, NWF = T::NWF, NT = T::NT, NPB = T::NPB;
+    constexpr int BBP = T::BBP, SPR = T::SPR;
+    constexpr int NWV = NT * NCH;
+    constexpr int PPW = (NPB + NWV - 1) / NWV;     // pieces per wave per block
+    // D blocks in flight plus two buffers: the one being read and the one the slowest wave
+    // may still have LDS reads outstanding on (a wave issues the DMA of block b + D after it
+    // passed the barrier of block b, so every wave has consumed block b - 2 by then)
+    constexpr int NBUF = D + 2;
+    constexpr int RCP = RC < 4 ? 4 : RC;
+    constexpr int NCW = RCP / 4;
+    constexpr int NST = RC * 8 * SPR;               // stores per wave per group
+    // PIPE: block b + 1's LDS reads are issued before block b is combined (register double
+    // buffer).  The compiled encode does without it: its constant XOR program already needs
+    // ~150 VGPRs, and a 10-wave workgroup must fit 3 waves per SIMD (<= 168 VGPRs, no spills).
+    constexpr bool PIPE = KC == 0;
+    constexpr int AHEAD = PIPE ? D - 1 : D;          // blocks issued after the awaited one
+    constexpr int WAITN = AHEAD * PPW;
+    constexpr int WAITG = AHEAD * PPW + NST > 63 ? 63 : AHEAD * PPW + NST;
+    constexpr int SAUX = DECODE ? 0 : 2;            // encode's dense parity stream: nt stores
+    static_assert(S % 2 == 0 && BB % 16 == 0, "16-byte aligned blocks, 2-byte aligned sub-rows");
+    static_assert(KC == 0 || (!DECODE && MC > 0 && (MC + RC - 1) / RC == NCH), "compiled code");
+    static_assert(WAITN <= 63 && D >= 2, "pipeline depth");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+    const int lane = threadIdx.x & 63;
+    const int w = wave_id();
+    const int tile = w % NT, chunk = w / NT;
+    const int c = min(tile * 64 + lane, NW - 1);     // idle lanes shadow the last word
+    if constexpr (KC > 0) {
+        k = KC;
+        m = MC;
+    }
+    const long long G0 = blockIdx.x, GS = gridDim.x;
+    if (G0 >= groups) return;                        // uniform over the workgroup
+    const long long cnt = (groups - 1 - G0) / GS + 1;
+    const long long nblocks = cnt * k;               // this workgroup's block stream
+
+    // ---- DMA side: block b of the stream = block iss_x of group G0 + iss_i * GS
+    long long iss_b = 0;
+    int iss_x = 0;
+    const uint8_t* iss_src = in + G0 * (long long)k * BB;
+    const long long gstride = GS * (long long)k * BB;
+    auto issue_next = [&]() {
+        uint8_t* dst = smem + (int)(iss_b % NBUF) * BBP;
+        const uint8_t* src = iss_src + (long long)iss_x * BB;
+#pragma unroll
+        for (int q = 0; q < PPW; ++q) {
+            const int p = min(w + q * NWV, NPB - 1);   // surplus waves reload the last piece
+            const int off = min(p * 1024 + lane * 16, BB - 16);
+            __builtin_amdgcn_global_load_lds(QT_GPTR(src + off), QT_LPTR(dst + p * 1024), 16, 0,
+                                             2);
+        }
+        ++iss_b;
+        if (++iss_x == k) {
+            iss_x = 0;
+            iss_src += gstride;
+        }
+    };
+
+    // ---- LDS side: column word c of the 8 sub-rows of block b (aligned dwords; sub-row t
+    // starts t * S bytes into the buffer, misaligned by (t * S) & 3, realigned at use)
+    auto read_block = [&](long long b, uint32_t (&lo)[8], uint32_t (&hi)[8]) {
+        uint32_t c4 = 4u * (uint32_t)c;
+        if constexpr (KC > 0) asm volatile("" : "+v"(c4));   // no hoisting across blocks
+        const uint8_t* L = smem + (int)(b % NBUF) * BBP + c4;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int o = t * S;
+            const uint32_t* q = (const uint32_t*)(L + (o & ~3));
+            lo[t] = q[0];
+            hi[t] = (o & 3) ? q[1] : 0u;
+        }
+    };
+    // wait for block bw's pieces (this wave's), then for every wave's
+    auto wait_block = [&](long long bw, bool after_stores) {
+        if (bw + AHEAD < nblocks) {
+            if (after_stores) tile_wait_vmcnt<WAITG>();
+            else tile_wait_vmcnt<WAITN>();
+        } else {
+            tile_wait_vmcnt<0>();   // stream tail: fewer younger pieces
+        }
+        tile_barrier();
+    };
+
+#pragma unroll 1
+    for (int u = 0; u < D; ++u)
+        if (u < nblocks) issue_next();
+    uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
+    if constexpr (PIPE) {
+        wait_block(0, false);
+        read_block(0, lo0, hi0);
+    }
+
+    long long b = 0;   // stream index of the current block
+#pragma unroll 1
+    for (long long i = 0; i < cnt; ++i) {
+        const long long g = G0 + i * GS;
+        int n;
+        if (DECODE) n = min(nout[g] - chunk * RC, RC);
+        else n = min(m - chunk * RC, RC);
+        const uint32_t* cw = (const uint32_t*)(coef + (DECODE ? g * coef_gstride : 0)) +
+                             (long long)chunk * k * NCW;
+        uint32_t acc[RC][8];
+#pragma unroll
+        for (int j = 0; j < RC; ++j)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) acc[j][r] = 0;
+
+        // one block: prefetch block b + D, pull block b + 1 into registers, combine block b
+        // xc: the block index in the group, an int or (KC > 0) an integral_constant;
+        // chc: the chunk (KC > 0: an integral_constant)
+        auto step = [&](auto xc, auto chc, uint32_t (&lo)[8], uint32_t (&hi)[8],
+                        uint32_t (&nlo)[8], uint32_t (&nhi)[8]) __attribute__((always_inline)) {
+            const int x = xc;
+            if (b + D < nblocks) issue_next();
+            // blocks 0 .. D - 1 of a group were DMA'd before the previous group's stores
+            // were issued, so those stores are younger than their pieces
+            if constexpr (PIPE) {
+                if (b + 1 < nblocks) {
+                    wait_block(b + 1, i > 0 && x + 1 <= D - 1);
+                    read_block(b + 1, nlo, nhi);
+                }
+            } else {
+                wait_block(b, i > 0 && x <= D - 1);
+                read_block(b, lo, hi);
+            }
+            ++b;
+            WZ v;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int o = t * S;
+                v.W[t] = (o & 3) ? __builtin_amdgcn_alignbyte(hi[t], lo[t], o & 3) : lo[t];
+            }
+            if constexpr (KC > 0) {
+                expand_wz(v);
+                constexpr int CH = decltype(chc)::value;
+                static_for<RC>([&](auto jc) __attribute__((always_inline)) {
+                    constexpr int o = CH * RC + decltype(jc)::value;
+                    if constexpr (o == 0) {
+                        // row 0 is P0, all coefficients 1 (cauchy_256.cpp:1519-1523)
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) acc[0][r] ^= v.W[r];
+                    } else if constexpr (o < MC) {
+                        constexpr uint32_t cf = cauchy_coef(MC, o, decltype(xc)::value);
+                        apply_nibble<0>(acc[decltype(jc)::value], cf & 15u, v);
+                        apply_nibble<4>(acc[decltype(jc)::value], cf >> 4, v);
+                    }
+                });
+            } else {
+                if (n <= 0) return;   // no output in this chunk for this group
+                uint32_t cwv[NCW];
+#pragma unroll
+                for (int q = 0; q < NCW; ++q) cwv[q] = cw[x * NCW + q];
+                expand_wz(v);
+#pragma unroll
+                for (int j = 0; j < RC; ++j) {
+                    if (j < n) {
+                        const uint32_t cf = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                        apply_nibble<0>(acc[j], cf & 15u, v);
+                        apply_nibble<4>(acc[j], cf >> 4, v);
+                    }
+                }
+            }
+        };
+        if constexpr (KC > 0) {
+            static_for<NCH>([&](auto chc) __attribute__((always_inline)) {
+                if (chunk == decltype(chc)::value) {
+                    static_for<KC>([&](auto xc) __attribute__((always_inline)) {
+                        // accumulators opaque at every block boundary: with constant
+                        // coefficients the XOR reassociation would otherwise merge the
+                        // blocks' sums into one tree and keep every block's W/Z live
+#pragma unroll
+                        for (int j = 0; j < RC; ++j)
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
+                        if constexpr (decltype(xc)::value % 2 == 0)
+                            step(xc, chc, lo0, hi0, lo1, hi1);
+                        else
+                            step(xc, chc, lo1, hi1, lo0, hi0);
+                    });
+                }
+            });
+            // KC is even: the next group's first block is in lo0/hi0 again
+            static_assert(KC % 2 == 0, "register double buffer parity");
+        } else {
+            // the run-time loop keeps the parity of the double buffer by steps of 2; an odd
+            // k leaves the next block in lo1/hi1, so it is swapped back
+#pragma unroll 1
+            for (int x = 0; x + 1 < k; x += 2) {
+                step(x, 0, lo0, hi0, lo1, hi1);
+                step(x + 1, 0, lo1, hi1, lo0, hi0);
+            }
+            if (k & 1) {
+                step(k - 1, 0, lo0, hi0, lo1, hi1);
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    lo0[t] = lo1[t];
+                    hi0[t] = hi1[t];
+                }
+            }
+        }
+
+        // ---- outputs: a fixed number of store instructions (unused outputs, idle lanes
+        // and the lanes outside a word's valid bytes are dropped)
+        const bool live = tile * 64 + lane < NW;
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+            const bool on = j < n;
+            const int o = chunk * RC + j;
+            const int oslot = (DECODE && slots) ? (on ? tile_sload_u8(slots, g * rmax + o) : 0)
+                                                : o;
+            uint8_t* dst = out + g * out_gstride + (long long)oslot * BB;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(dst, 0, (unsigned)BB, 0x00020000);
+            const bool tail = live && c == NWF && NWF < NW;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const uint32_t vsum = acc[j][r];
+                const unsigned at = (unsigned)(r * S + 4 * c);
+                __builtin_amdgcn_raw_buffer_store_b32(vsum, rs, on && live && c < NWF ? at : kTDrop,
+                                                      0, SAUX);
+                if (S & 2)
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)vsum, rs,
+                                                          on && tail ? at : kTDrop, 0, SAUX);
+                if (S & 1)
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(vsum >> (8 * (S & 2))), rs,
+                                                         on && tail ? at + (S & 2) : kTDrop, 0,
+                                                         SAUX);
+            }
+        }
+    }
+    tile_wait_vmcnt<0>();
+}
+
+namespace {
+constexpr int kTileS = 1126;   // bb = 9008: 9000-byte payloads (BASELINE config D)
+constexpr int kTileD = 6;      // blocks in flight per workgroup
+}  // namespace
+
+bool gf_tile_supported(int k, int m, int bb, int rc, bool decode, const Tune& t) {
+    (void)k;
+    if (!t.tile) return false;
+    if (bb != 8 * kTileS || rc != 8 || k < kTileD + 2) return false;
+    // encode: the compiled code only (the run-time form of this kernel spills at the
+    // 10-wave occupancy it needs; other codes stay on gf_apply)
+    if (!decode) return t.const_enc && k == 128 && m == 16;
+    return (std::min(k, m) + rc - 1) / rc <= 2;
+}
+
+hipError_t launch_gf_tile(const uint8_t* in, uint8_t* out, const uint8_t* coef,
+                          const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
+                          long long groups, int rc, int rmax, long long coef_gstride,
+                          long long out_gstride, bool decode, hipStream_t st, const Tune& t) {
+    if (groups <= 0) return hipSuccess;
+    if (!gf_tile_supported(k, m, bb, rc, decode, t)) return hipErrorInvalidValue;
+    if (((uintptr_t)in & 15) != 0 || ((uintptr_t)slots & 3) != 0) return hipErrorInvalidValue;
+    using TS = TileShape<kTileS>;
+    const int nch = ((decode ? rmax : m) + rc - 1) / rc;
+    const size_t lds = (size_t)(kTileD + 2) * TS::BBP;
+    const unsigned threads = (unsigned)(TS::NT * nch * 64);
+    // workgroups per CU: LDS and 16 waves (the kernels use <= 128 VGPRs)
+    const int per_cu = std::max(1, std::min((int)((160 * 1024) / lds), 16 / (TS::NT * nch)));
+    long long cap = (long long)t.cus * per_cu;
+    if (t.tile_grid > 0) cap = t.tile_grid;              // tests: many groups per workgroup
+    const unsigned grid = (unsigned)std::min<long long>(groups, cap);
+#define QT_GO(NCHV, DEC, KCV, MCV)                                                              \
+    hipLaunchKernelGGL((gf_tile_kernel<kTileS, 8, NCHV, DEC, kTileD, KCV, MCV>), dim3(grid),     \
+                       dim3(threads), lds, st, in, out, coef, slots, nout, groups, k, m, rmax,  \
+                       coef_gstride, out_gstride)
+    if (decode) {
+        note_kernel("gf_tile_kernel<decode>");
+        if (nch == 1) QT_GO(1, true, 0, 0);
+        else QT_GO(2, true, 0, 0);
+    } else {
+        note_kernel("gf_tile_kernel<encode,k128m16>");
+        QT_GO(2, false, 128, 16);
+    }
+#undef QT_GO
+    return hipGetLastError();
+}
+
+}  // namespace qfec

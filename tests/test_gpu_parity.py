@@ -126,6 +126,8 @@ CONFIGS = [
     (17, 5, 1352, 5, True), (16, 8, 9008, 8, False), (20, 10, 64, 10, True),
     (128, 16, 1352, 8, False), (100, 20, 136, 17, True), (40, 40, 32, 33, True),
     (200, 56, 16, 40, False), (250, 5, 1352, 5, False), (10, 15, 1352, 10, True),
+    (128, 16, 9008, 8, True), (128, 16, 9008, 16, False), (130, 16, 9008, 3, True),
+    (8, 5, 9008, 5, False),
 ]
 
 
@@ -391,7 +393,7 @@ OPTION_SETS = [
     {"xor_slots": 3, "xor_waves": 3}, {"xor_slots": 4, "xor_waves": 2}, {"xor_waves": 1},
     {"dma": 0}, {"stream": 0}, {"stream": 0, "pd": 1}, {"stream": 0, "pd": 3},
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
-    {"stream_ring": 36}, {"host_chunk_mb": 1}, {"const_enc": 0},
+    {"stream_ring": 36}, {"host_chunk_mb": 1}, {"const_enc": 0}, {"tile": 0},
 ]
 
 
@@ -602,6 +604,46 @@ def test_stream_any_small_block(engine, oracle, bb, k, m, r):
     rec_rows = torch.zeros((G, rmax), dtype=torch.uint8, device="cuda")
     engine.decode_recovered(k, m, bb, dev(recv), dev(rows), rec, rec_rows)
     assert "gf_stream_kernel<decode" in fec.last_kernels()
+    np.testing.assert_array_equal(host(rec_rows), exp_rows)
+    mask = exp_rows != 255
+    np.testing.assert_array_equal(host(rec)[mask], exp[mask])
+
+
+# ------------------------------------------------- gf_tile (9008-byte blocks, config D)
+@pytest.mark.parametrize("grid", [1, 3, 0])
+@pytest.mark.parametrize("k,m,r", [(128, 16, 8), (128, 16, 13), (40, 16, 16), (9, 6, 4)])
+def test_tile_many_groups_per_workgroup(tuned_engine, oracle, grid, k, m, r):
+    """Config D's kernel with the grid capped so one workgroup streams several groups back
+    to back (the DMA prefetch crosses group boundaries and the previous group's stores sit
+    in the vmcnt count); every third group has no loss."""
+    import torch
+    engine = tuned_engine
+    engine.set_option("tile_grid", grid)
+    bb, G = 9008, 7
+    data = synth.group_data(4000 + k + m + grid, k, bb, G)
+    p_or, rc_or = oracle.encode_batch(k, m, bb, data)
+    p_gpu, rc = gpu_encode(engine, k, m, bb, data)
+    if (k, m) == (128, 16):
+        assert fec.last_kernels() == "gf_tile_kernel<encode,k128m16>"
+    assert rc == rc_or == 0
+    np.testing.assert_array_equal(p_gpu, p_or)
+    rows, src = synth.loss_patterns(k, m, r, G, 71 + grid, shuffle=True)
+    rows[::3] = np.arange(k, dtype=rows.dtype)
+    src[::3] = np.arange(k, dtype=src.dtype)
+    recv = synth.assemble_received(data, p_or, src)
+    b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+    for inplace in (True, False):
+        b, rr, s = gpu_decode(engine, k, m, bb, recv, rows, inplace=inplace)
+        assert "gf_tile_kernel<decode>" in fec.last_kernels()
+        np.testing.assert_array_equal(s, s_or)
+        np.testing.assert_array_equal(rr, r_or)
+        np.testing.assert_array_equal(b, b_or)
+    exp, exp_rows = expected_recovered(k, m, bb, rows, b_or, r_or, s_or)
+    rmax = min(k, m)
+    rec = torch.zeros((G, rmax, bb), dtype=torch.uint8, device="cuda")
+    rec_rows = torch.zeros((G, rmax), dtype=torch.uint8, device="cuda")
+    engine.decode_recovered(k, m, bb, dev(recv), dev(rows), rec, rec_rows)
+    assert "gf_tile_kernel<decode>" in fec.last_kernels()
     np.testing.assert_array_equal(host(rec_rows), exp_rows)
     mask = exp_rows != 255
     np.testing.assert_array_equal(host(rec)[mask], exp[mask])

@@ -1,10 +1,11 @@
 """ISA guard for the counted-vmcnt kernels (CPU only: hipcc cross-compiles gfx950).
 
-gf_stream_kernel (quic_amd/csrc/gf_stream.hip) keeps its own count of the VMEM
-instructions it issued and waits with `s_waitcnt vmcnt(N)` for exactly the pieces a
-block needs.  That is only sound if the compiler emits no VMEM instruction outside the
-count (a global_load of a uniform byte, say) and inserts no vmcnt wait of its own (which
-would drain the ring).  This test compiles the file and checks both."""
+gf_stream_kernel (quic_amd/csrc/gf_stream.hip) and gf_tile_kernel (gf_tile.hip) keep their
+own count of the VMEM instructions they issued and wait with `s_waitcnt vmcnt(N)` for
+exactly the pieces a block needs.  That is only sound if the compiler emits no VMEM
+instruction outside the count (a global_load of a uniform byte, a register spill, say) and
+inserts no vmcnt wait of its own (which would drain the pipeline).  This test compiles the
+files and checks both."""
 import os
 import re
 import subprocess
@@ -17,25 +18,28 @@ COUNTED = {"global_load_lds_dwordx4", "buffer_store_dword", "buffer_store_short"
            "buffer_store_byte"}
 
 
-@pytest.fixture(scope="module")
-def stream_isa(tmp_path_factory):
+@pytest.fixture(scope="module", params=["gf_stream", "gf_tile"])
+def stream_isa(tmp_path_factory, request):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
-    out = tmp_path_factory.mktemp("isa") / "gf_stream.s"
-    src = os.path.join(ROOT, "quic_amd", "csrc", "gf_stream.hip")
+    name = request.param
+    out = tmp_path_factory.mktemp("isa") / f"{name}.s"
+    src = os.path.join(ROOT, "quic_amd", "csrc", f"{name}.hip")
     subprocess.run(["python3", os.path.join(ROOT, "tools", "gen_cauchy_const.py")], check=True,
                    capture_output=True)
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17",
                     "-mllvm", "-structurizecfg-skip-uniform-regions=true", "-DQFEC_BUILD",
                     "-I", os.path.join(ROOT, "build", "gen"),
+                    "-I", os.path.join(ROOT, "quic_amd", "csrc"),
                     "--cuda-device-only", "-S", "-o", str(out), src],
                    check=True, capture_output=True)
     text = out.read_text()
     bodies = {}
-    for m in re.finditer(r"^(_ZN4qfec16gf_stream_kernel\w+):", text, re.M):
+    for m in re.finditer(r"^(_ZN4qfec\d+" + name + r"_kernel\w+):", text, re.M):
         end = text.index(".Lfunc_end", m.end())
         bodies[m.group(1)] = text[m.end():end]
-    assert len(bodies) >= 6, "expected RC 2/4/8 x encode/decode instantiations"
+    assert len(bodies) >= 3, "expected the encode and decode instantiations"
+    assert not re.search(r"\.private_segment_fixed_size:\s+[1-9]", text), "register spills"
     return bodies
 
 
