@@ -9,6 +9,8 @@
 
 #include <utility>
 
+#include "gf256.h"
+
 namespace qfec {
 
 // f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): a loop whose index is
@@ -38,7 +40,10 @@ __device__ __forceinline__ int wave_id() {
 // contributes  out[r] ^= XOR_{b : a_b} W[b + r]   (r = 0..7), i.e. per nibble p of a at
 // bit offset B a fixed XOR of at most two W/Z terms per output sub-row.
 struct WZ {
-    uint32_t W[15];
+    union {
+        uint32_t W[15];
+        uint32_t W8[8];   // the block's own 8 sub-row words (W[0..7])
+    };
     uint32_t Z[14];
 };
 
@@ -76,6 +81,62 @@ __device__ __forceinline__ void apply_nibble(uint32_t (&acc)[8], uint32_t p, con
         default: break;
     }
 #undef QF_CASE
+}
+
+// ------------------------------------------------ windowed form, compile-time coefficients
+// The reference's windowed encoder (cauchy_256.cpp:1419-1500, win_encode) splits a block's
+// 8 sub-rows into two groups of 4 and precomputes every XOR combination of each group; an
+// output sub-row r of coefficient c then needs the combination selected by the low nibble
+// of c * alpha^r plus the one selected by its high nibble.  With the coefficient known at
+// compile time that is ONE v_bitop3 per (output, sub-row) (acc ^ lo[M & 15] ^ hi[M >> 4]),
+// against two in the W/Z nibble form above; the compiler drops every combination no output
+// of the block uses.  Bit-exact with the W/Z form: both compute XOR_{t in bits(c alpha^r)}.
+struct Win {
+    uint32_t lo[16];   // lo[i] = XOR of in[t] for the set bits t of i      (t = 0..3)
+    uint32_t hi[16];   // hi[i] = XOR of in[4 + t] for the set bits t of i  (t = 0..3)
+};
+
+__device__ __forceinline__ void win_group(const uint32_t* in, uint32_t (&o)[16]) {
+    o[0] = 0;
+    o[1] = in[0];
+    o[2] = in[1];
+    o[3] = in[0] ^ in[1];
+    o[4] = in[2];
+    o[5] = in[0] ^ in[2];
+    o[6] = in[1] ^ in[2];
+    o[7] = xor3(in[0], in[1], in[2]);
+    o[8] = in[3];
+    o[9] = in[0] ^ in[3];
+    o[10] = in[1] ^ in[3];
+    o[11] = xor3(in[0], in[1], in[3]);
+    o[12] = in[2] ^ in[3];
+    o[13] = xor3(in[0], in[2], in[3]);
+    o[14] = xor3(in[1], in[2], in[3]);
+    o[15] = o[3] ^ o[12];
+}
+
+__device__ __forceinline__ void win_build(const uint32_t (&in)[8], Win& w) {
+    win_group(in, w.lo);
+    win_group(in + 4, w.hi);
+}
+
+constexpr uint8_t gf_alpha_pow(int r) {
+    uint8_t v = 1;
+    for (int i = 0; i < r; ++i) v = gf_xtime(v);
+    return v;
+}
+
+// acc[r] ^= (c * alpha^r) applied to the block, r = 0..7, for a compile-time coefficient C
+template <unsigned C>
+__device__ __forceinline__ void win_apply(uint32_t (&acc)[8], const Win& w) {
+    static_for<8>([&](auto rc) __attribute__((always_inline)) {
+        constexpr int r = decltype(rc)::value;
+        constexpr unsigned M = gf_mul((uint8_t)C, gf_alpha_pow(r));
+        constexpr unsigned a = M & 15u, b = M >> 4;
+        if constexpr (a && b) acc[r] = xor3(acc[r], w.lo[a], w.hi[b]);
+        else if constexpr (a) acc[r] ^= w.lo[a];
+        else if constexpr (b) acc[r] ^= w.hi[b];
+    });
 }
 
 }  // namespace qfec

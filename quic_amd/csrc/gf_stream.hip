@@ -224,24 +224,21 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     v.W[t] = (S == 0 || (o & 3)) ? __builtin_amdgcn_alignbyte(hi[t], lo[t], o & 3)
                                                  : lo[t];
                 }
-                uint32_t cwv[NCW];
-                if constexpr (KC == 0) {
-#pragma unroll
-                    for (int q = 0; q < NCW; ++q) cwv[q] = cw[x * NCW + q];
-                }
-                expand_wz(v);
                 if constexpr (KC > 0) {
-                    // row 0 is P0 (all ones); rows 1..m-1 with their compile-time coefficient
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) acc[0][r] ^= v.W[r];
-                    static_for<RC - 1>([&](auto jc) {
-                        constexpr int j = decltype(jc)::value + 1;
-                        constexpr uint32_t cf = cauchy_coef_small(RC, j, decltype(xc)::value);
-                        apply_nibble<0>(acc[j], cf & 15u, v);
-                        apply_nibble<4>(acc[j], cf >> 4, v);
+                    // windowed form (gf_bitslice.h): one v_bitop3 per (output, sub-row); row 0
+                    // is P0, all coefficients 1 (cauchy_256.cpp:1519-1523)
+                    Win win;
+                    win_build(v.W8, win);
+                    static_for<RC>([&](auto jc) __attribute__((always_inline)) {
+                        constexpr int j = decltype(jc)::value;
+                        win_apply<cauchy_coef_small(RC, j, decltype(xc)::value)>(acc[j], win);
                     });
                     return;
                 }
+                uint32_t cwv[NCW];
+#pragma unroll
+                for (int q = 0; q < NCW; ++q) cwv[q] = cw[x * NCW + q];
+                expand_wz(v);
 #pragma unroll
                 for (int j = 0; j < RC; ++j) {
                     if (!DECODE && j == 0) {
@@ -276,7 +273,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     if (x + 1 < k) step(x + 1, lo1, hi1, lo0, hi0);
                 }
             }
-            // ---- outputs: fixed instruction count per output (dropped lanes, no branches)
+            // ---- outputs: fixed instruction count per output (dropped lanes, no branches).
+            // Lane offsets 4c (full words) and the tail lane's, sub-row in the scalar offset:
+            // two address VGPRs, opaque so they are not hoisted as 8 x RC precomputed ones.
+            uint32_t vo = lane < NWF ? 4u * (uint32_t)c : kSDrop;
+            uint32_t vt = lane == NWF && NWF < NW ? 4u * (uint32_t)c : kSDrop;
+            asm volatile("" : "+v"(vo), "+v"(vt));
 #pragma unroll
             for (int j = 0; j < RC; ++j) {
                 if (j < n) {
@@ -284,20 +286,17 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     uint8_t* dst = out + g * out_gstride + (long long)oslot * BB;
                     const __amdgpu_buffer_rsrc_t rs =
                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, (unsigned)BB, 0x00020000);
-                    const bool tail = lane == NWF && NWF < NW;
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
                         const uint32_t vsum = acc[j][r];
-                        const unsigned at = (unsigned)(r * s + 4 * c);
-                        __builtin_amdgcn_raw_buffer_store_b32(vsum, rs, lane < NWF ? at : kSDrop,
-                                                              0, SAUX);
+                        __builtin_amdgcn_raw_buffer_store_b32(vsum, rs, vo, r * s, SAUX);
                         if (S == 0 || (S & 2))
                             __builtin_amdgcn_raw_buffer_store_b16(
-                                (uint16_t)vsum, rs, tail && (s & 2) ? at : kSDrop, 0, SAUX);
+                                (uint16_t)vsum, rs, (s & 2) ? vt : kSDrop, r * s, SAUX);
                         if (S == 0 || (S & 1))
                             __builtin_amdgcn_raw_buffer_store_b8(
-                                (uint8_t)(vsum >> (8 * (s & 2))), rs,
-                                tail && (s & 1) ? at + (s & 2) : kSDrop, 0, SAUX);
+                                (uint8_t)(vsum >> (8 * (s & 2))), rs, (s & 1) ? vt : kSDrop,
+                                r * s + (s & 2), SAUX);
                     }
                     vm += 8 * SPR;
                 }

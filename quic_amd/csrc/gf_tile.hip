@@ -69,7 +69,8 @@ struct TileShape {
 // S: sub-row bytes (compile time).  RC: outputs per chunk wave, NCH chunks.  D: blocks in
 // flight (D + 2 LDS buffers).  KC, MC > 0: encode of the compiled code (k, m) = (KC, MC).
 template <int S, int RC, int NCH, bool DECODE, int D, int KC = 0, int MC = 0>
-__global__ __launch_bounds__(TileShape<S>::NT * NCH * 64, 3) void gf_tile_kernel(
+__global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
+                             (TileShape<S>::NT * NCH + 3) / 4) void gf_tile_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
     int k, int m, int rmax, long long coef_gstride, long long out_gstride) {
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64, 3) void gf_tile_kernel
     // PIPE: block b + 1's LDS reads are issued before block b is combined (register double
     // buffer).  The compiled encode does without it: its constant XOR program already needs
     // ~150 VGPRs, and a 10-wave workgroup must fit 3 waves per SIMD (<= 168 VGPRs, no spills).
-    constexpr bool PIPE = KC == 0;
+    constexpr bool PIPE = true;
     constexpr int AHEAD = PIPE ? D - 1 : D;          // blocks issued after the awaited one
     constexpr int WAITN = AHEAD * PPW;
     constexpr int WAITG = AHEAD * PPW + NST > 63 ? 63 : AHEAD * PPW + NST;
@@ -171,11 +172,15 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64, 3) void gf_tile_kernel
 #pragma unroll 1
     for (long long i = 0; i < cnt; ++i) {
         const long long g = G0 + i * GS;
+        // Encode: chunk c owns outputs c * RC + j.  Decode interleaves them, output
+        // o = NCH * j + c, so that with fewer than NCH * RC erasures every chunk's waves still
+        // share the work (8 losses of a (128, 16) group: 4 outputs each, not 8 and 0).
         int n;
-        if (DECODE) n = min(nout[g] - chunk * RC, RC);
+        if (DECODE) n = min((nout[g] - chunk + NCH - 1) / NCH, RC);
         else n = min(m - chunk * RC, RC);
+        // decode prep table [G][nchunk][k][RCP]: output o is byte o % RC of chunk o / RC
         const uint32_t* cw = (const uint32_t*)(coef + (DECODE ? g * coef_gstride : 0)) +
-                             (long long)chunk * k * NCW;
+                             (DECODE ? 0 : (long long)chunk * k * NCW);
         uint32_t acc[RC][8];
 #pragma unroll
         for (int j = 0; j < RC; ++j)
@@ -208,30 +213,46 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64, 3) void gf_tile_kernel
                 v.W[t] = (o & 3) ? __builtin_amdgcn_alignbyte(hi[t], lo[t], o & 3) : lo[t];
             }
             if constexpr (KC > 0) {
-                expand_wz(v);
-                constexpr int CH = decltype(chc)::value;
-                static_for<RC>([&](auto jc) __attribute__((always_inline)) {
-                    constexpr int o = CH * RC + decltype(jc)::value;
-                    if constexpr (o == 0) {
-                        // row 0 is P0, all coefficients 1 (cauchy_256.cpp:1519-1523)
-#pragma unroll
-                        for (int r = 0; r < 8; ++r) acc[0][r] ^= v.W[r];
-                    } else if constexpr (o < MC) {
-                        constexpr uint32_t cf = cauchy_coef(MC, o, decltype(xc)::value);
-                        apply_nibble<0>(acc[decltype(jc)::value], cf & 15u, v);
-                        apply_nibble<4>(acc[decltype(jc)::value], cf >> 4, v);
+                // windowed form (gf_bitslice.h): one v_bitop3 per (output, sub-row); row 0 is
+                // P0, all coefficients 1 (cauchy_256.cpp:1519-1523)
+                // The blocks' common work (DMA, waits, LDS reads, the combinations) is
+                // shared; only the apply differs per chunk, behind a uniform branch.
+                Win win;
+                win_build(v.W8, win);
+                static_for<NCH>([&](auto chc2) __attribute__((always_inline)) {
+                    constexpr int CH = decltype(chc2)::value;
+                    if (chunk == CH) {
+                        static_for<RC>([&](auto jc) __attribute__((always_inline)) {
+                            constexpr int o = CH * RC + decltype(jc)::value;
+                            if constexpr (o < MC)
+                                win_apply<cauchy_coef(MC, o, decltype(xc)::value)>(
+                                    acc[decltype(jc)::value], win);
+                        });
                     }
                 });
+                (void)chc;
             } else {
                 if (n <= 0) return;   // no output in this chunk for this group
-                uint32_t cwv[NCW];
+                // coefficient rows of block x in every chunk: NCH x NCW dwords
+                uint32_t cwv[NCH][NCW];
 #pragma unroll
-                for (int q = 0; q < NCW; ++q) cwv[q] = cw[x * NCW + q];
+                for (int h = 0; h < NCH; ++h)
+#pragma unroll
+                    for (int q = 0; q < NCW; ++q)
+                        cwv[h][q] = cw[((long long)h * k + x) * NCW + q];
                 expand_wz(v);
 #pragma unroll
                 for (int j = 0; j < RC; ++j) {
                     if (j < n) {
-                        const uint32_t cf = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                        const int o = NCH * j + chunk;             // wave-uniform
+                        const int h = o / RC, pos = o % RC;
+                        uint32_t word = cwv[0][0];
+#pragma unroll
+                        for (int hh = 0; hh < NCH; ++hh)
+#pragma unroll
+                            for (int q = 0; q < NCW; ++q)
+                                if (hh == h && q == (pos >> 2)) word = cwv[hh][q];
+                        const uint32_t cf = (word >> (8 * (pos & 3))) & 0xFFu;
                         apply_nibble<0>(acc[j], cf & 15u, v);
                         apply_nibble<4>(acc[j], cf >> 4, v);
                     }
@@ -239,22 +260,20 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64, 3) void gf_tile_kernel
             }
         };
         if constexpr (KC > 0) {
-            static_for<NCH>([&](auto chc) __attribute__((always_inline)) {
-                if (chunk == decltype(chc)::value) {
-                    static_for<KC>([&](auto xc) __attribute__((always_inline)) {
-                        // accumulators opaque at every block boundary: with constant
-                        // coefficients the XOR reassociation would otherwise merge the
-                        // blocks' sums into one tree and keep every block's W/Z live
+            static_for<KC>([&](auto xc) __attribute__((always_inline)) {
+                // accumulators opaque at every block boundary: with constant coefficients
+                // the XOR reassociation would otherwise merge the blocks' sums into one tree
+                // and keep every block's combinations live
 #pragma unroll
-                        for (int j = 0; j < RC; ++j)
+                for (int j = 0; j < RC; ++j)
 #pragma unroll
-                            for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
-                        if constexpr (decltype(xc)::value % 2 == 0)
-                            step(xc, chc, lo0, hi0, lo1, hi1);
-                        else
-                            step(xc, chc, lo1, hi1, lo0, hi0);
-                    });
-                }
+                    for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
+                // and no instruction scheduled across blocks (register pressure)
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (decltype(xc)::value % 2 == 0)
+                    step(xc, 0, lo0, hi0, lo1, hi1);
+                else
+                    step(xc, 0, lo1, hi1, lo0, hi0);
             });
             // KC is even: the next group's first block is in lo0/hi0 again
             static_assert(KC % 2 == 0, "register double buffer parity");
@@ -278,30 +297,32 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64, 3) void gf_tile_kernel
 
         // ---- outputs: a fixed number of store instructions (unused outputs, idle lanes
         // and the lanes outside a word's valid bytes are dropped)
+        // Lane offsets: 4c for the full words, the tail word's lane, everyone else dropped;
+        // the sub-row goes into the scalar offset and an unused output gets an empty range,
+        // so the whole phase needs two VGPRs of addresses (opaque: not hoisted out of the
+        // group loop as 8 x RC precomputed offsets).
         const bool live = tile * 64 + lane < NW;
+        uint32_t vo = live && c < NWF ? 4u * (uint32_t)c : kTDrop;
+        uint32_t vt = live && c == NWF && NWF < NW ? 4u * (uint32_t)c : kTDrop;
+        asm volatile("" : "+v"(vo), "+v"(vt));
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
             const bool on = j < n;
-            const int o = chunk * RC + j;
+            const int o = DECODE ? NCH * j + chunk : chunk * RC + j;
             const int oslot = (DECODE && slots) ? (on ? tile_sload_u8(slots, g * rmax + o) : 0)
                                                 : o;
             uint8_t* dst = out + g * out_gstride + (long long)oslot * BB;
             const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(dst, 0, (unsigned)BB, 0x00020000);
-            const bool tail = live && c == NWF && NWF < NW;
+                __builtin_amdgcn_make_buffer_rsrc(dst, 0, on ? (unsigned)BB : 0u, 0x00020000);
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
                 const uint32_t vsum = acc[j][r];
-                const unsigned at = (unsigned)(r * S + 4 * c);
-                __builtin_amdgcn_raw_buffer_store_b32(vsum, rs, on && live && c < NWF ? at : kTDrop,
-                                                      0, SAUX);
+                __builtin_amdgcn_raw_buffer_store_b32(vsum, rs, vo, r * S, SAUX);
                 if (S & 2)
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)vsum, rs,
-                                                          on && tail ? at : kTDrop, 0, SAUX);
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)vsum, rs, vt, r * S, SAUX);
                 if (S & 1)
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(vsum >> (8 * (S & 2))), rs,
-                                                         on && tail ? at + (S & 2) : kTDrop, 0,
-                                                         SAUX);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(vsum >> (8 * (S & 2))), rs, vt,
+                                                         r * S + (S & 2), SAUX);
             }
         }
     }
@@ -331,7 +352,7 @@ hipError_t launch_gf_tile(const uint8_t* in, uint8_t* out, const uint8_t* coef,
     if (!gf_tile_supported(k, m, bb, rc, decode, t)) return hipErrorInvalidValue;
     if (((uintptr_t)in & 15) != 0 || ((uintptr_t)slots & 3) != 0) return hipErrorInvalidValue;
     using TS = TileShape<kTileS>;
-    const int nch = ((decode ? rmax : m) + rc - 1) / rc;
+    const int nch = decode ? (rmax + rc - 1) / rc : (t.tile_chunks == 3 ? 3 : 2);
     const size_t lds = (size_t)(kTileD + 2) * TS::BBP;
     const unsigned threads = (unsigned)(TS::NT * nch * 64);
     // workgroups per CU: LDS and 16 waves (the kernels use <= 128 VGPRs)
@@ -347,6 +368,12 @@ hipError_t launch_gf_tile(const uint8_t* in, uint8_t* out, const uint8_t* coef,
         note_kernel("gf_tile_kernel<decode>");
         if (nch == 1) QT_GO(1, true, 0, 0);
         else QT_GO(2, true, 0, 0);
+    } else if (t.tile_chunks == 3) {
+        // 15 waves (4 per SIMD but one): 3 chunks of 6 outputs
+        note_kernel("gf_tile_kernel<encode,k128m16,3x6>");
+        hipLaunchKernelGGL((gf_tile_kernel<kTileS, 6, 3, false, kTileD, 128, 16>), dim3(grid),
+                           dim3(TS::NT * 3 * 64), lds, st, in, out, coef, slots, nout, groups, k,
+                           m, rmax, coef_gstride, out_gstride);
     } else {
         note_kernel("gf_tile_kernel<encode,k128m16>");
         QT_GO(2, false, 128, 16);
