@@ -320,6 +320,8 @@ def main():
                          "on several")
     ap.add_argument("--groups", type=int, default=None,
                     help="groups per GPU (A/B/D) or in total (C); default: the BASELINE size")
+    ap.add_argument("--losses", type=int, default=None,
+                    help="data blocks lost per group (default: the workload's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-groups", type=int, default=None,
                     help="groups per thread in the CPU sample (default: about 8 MB of data "
@@ -370,6 +372,8 @@ def main():
     from quic_amd import fec, shard, synth
     wname = args.workload or ("A" if world == 1 else "C")
     k, m, payload, r, groups_dflt, strong = WORKLOADS[wname]
+    if args.losses is not None:
+        r = args.losses
     groups_arg = args.groups if args.groups is not None else groups_dflt
     bb = block_bytes(payload)
     if strong:

@@ -511,14 +511,16 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"dma", &t.dma, 0, 1},                 {"stream", &t.stream, 0, 1},
         {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
         {"const_enc", &t.const_enc, 0, 1},     {"tile", &t.tile, 0, 1},
-        {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_chunks", &t.tile_chunks, 2, 3},
+        {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_depth", &t.tile_depth, 6, 12},
+        {"tile_rot", &t.tile_rot, 0, 255},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
     };
     for (const Opt& o : opts) {
         if (strcmp(o.n, name) != 0) continue;
-        if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))))
+        if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))) ||
+            (o.p == &t.tile_depth && value != 6 && value != 12))
             return fail(-2, std::string("option value out of range: ") + name);
         *o.p = value;
         return 0;
@@ -534,7 +536,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
         {"const_enc", t.const_enc}, {"tile", t.tile}, {"tile_grid", t.tile_grid},
-        {"tile_chunks", t.tile_chunks},
+        {"tile_depth", t.tile_depth}, {"tile_rot", t.tile_rot},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb},
     };

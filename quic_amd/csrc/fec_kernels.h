@@ -26,7 +26,8 @@ struct Tune {
     int const_enc = 1;        // encode kernels specialised for fixed (k, m) where compiled
     int tile = 1;             // m > 1, 9008-byte blocks: gf_tile (0: gf_apply)
     int tile_grid = 0;        // gf_tile: grid cap in workgroups (0: CUs x per-CU fit)
-    int tile_chunks = 2;      // gf_tile compiled encode: output chunks (2 x 8 or 3 x 6)
+    int tile_depth = 6;       // gf_tile: blocks in flight per workgroup (6 or 12)
+    int tile_rot = 37;        // gf_tile decode: per-workgroup block rotation multiplier
     int pd = 2;               // gf_apply: register pipeline depth (1..3)
     int flat = 1;             // gf_apply: lane-flat encode
     int enc_rc = 8;           // gf_apply: encode outputs per wave (2, 4, 8)

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
                              (TileShape<S>::NT * NCH + 3) / 4) void gf_tile_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
-    int k, int m, int rmax, long long coef_gstride, long long out_gstride) {
+    int k, int m, int rmax, long long coef_gstride, long long out_gstride, int rot_mul) {
     using T = TileShape<S>;
     constexpr int BB = T::BB, NW = T::NW, NWF = T::NWF, NT = T::NT, NPB = T::NPB;
     constexpr int BBP = T::BBP, SPR = T::SPR;
@@ -112,14 +112,19 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
     const long long cnt = (groups - 1 - G0) / GS + 1;
     const long long nblocks = cnt * k;               // this workgroup's block stream
 
-    // ---- DMA side: block b of the stream = block iss_x of group G0 + iss_i * GS
+    // ---- DMA side: block b of the stream = block (iss_x + rot) % k of group G0 + iss_i * GS.
+    // The run-time form may start every group at a per-workgroup block offset `rot`: the
+    // concurrently streamed groups are 1,153,024 B = 2^11 * 563 apart, so without it every
+    // workgroup reads the same offset of its group at the same time.
+    const int rot = KC > 0 ? 0 : (int)(((long long)G0 * rot_mul) % k);
     long long iss_b = 0;
     int iss_x = 0;
     const uint8_t* iss_src = in + G0 * (long long)k * BB;
     const long long gstride = GS * (long long)k * BB;
     auto issue_next = [&]() {
         uint8_t* dst = smem + (int)(iss_b % NBUF) * BBP;
-        const uint8_t* src = iss_src + (long long)iss_x * BB;
+        const int xm = iss_x + rot < k ? iss_x + rot : iss_x + rot - k;
+        const uint8_t* src = iss_src + (long long)xm * BB;
 #pragma unroll
         for (int q = 0; q < PPW; ++q) {
             const int p = min(w + q * NWV, NPB - 1);   // surplus waves reload the last piece
@@ -239,7 +244,7 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
                 for (int h = 0; h < NCH; ++h)
 #pragma unroll
                     for (int q = 0; q < NCW; ++q)
-                        cwv[h][q] = cw[((long long)h * k + x) * NCW + q];
+                        cwv[h][q] = cw[((long long)h * k + (x + rot < k ? x + rot : x + rot - k)) * NCW + q];
                 expand_wz(v);
 #pragma unroll
                 for (int j = 0; j < RC; ++j) {
@@ -331,13 +336,11 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
 
 namespace {
 constexpr int kTileS = 1126;   // bb = 9008: 9000-byte payloads (BASELINE config D)
-constexpr int kTileD = 6;      // blocks in flight per workgroup
 }  // namespace
 
 bool gf_tile_supported(int k, int m, int bb, int rc, bool decode, const Tune& t) {
-    (void)k;
     if (!t.tile) return false;
-    if (bb != 8 * kTileS || rc != 8 || k < kTileD + 2) return false;
+    if (bb != 8 * kTileS || rc != 8 || k < t.tile_depth + 2) return false;
     // encode: the compiled code only (the run-time form of this kernel spills at the
     // 10-wave occupancy it needs; other codes stay on gf_apply)
     if (!decode) return t.const_enc && k == 128 && m == 16;
@@ -351,33 +354,34 @@ hipError_t launch_gf_tile(const uint8_t* in, uint8_t* out, const uint8_t* coef,
     if (groups <= 0) return hipSuccess;
     if (!gf_tile_supported(k, m, bb, rc, decode, t)) return hipErrorInvalidValue;
     if (((uintptr_t)in & 15) != 0 || ((uintptr_t)slots & 3) != 0) return hipErrorInvalidValue;
+    if (t.tile_depth != 6 && t.tile_depth != 12) return hipErrorInvalidValue;
     using TS = TileShape<kTileS>;
-    const int nch = decode ? (rmax + rc - 1) / rc : (t.tile_chunks == 3 ? 3 : 2);
-    const size_t lds = (size_t)(kTileD + 2) * TS::BBP;
+    const int nch = decode ? (rmax + rc - 1) / rc : 2;
+    const size_t lds = (size_t)(t.tile_depth + 2) * TS::BBP;
     const unsigned threads = (unsigned)(TS::NT * nch * 64);
     // workgroups per CU: LDS and 16 waves (the kernels use <= 128 VGPRs)
     const int per_cu = std::max(1, std::min((int)((160 * 1024) / lds), 16 / (TS::NT * nch)));
     long long cap = (long long)t.cus * per_cu;
     if (t.tile_grid > 0) cap = t.tile_grid;              // tests: many groups per workgroup
     const unsigned grid = (unsigned)std::min<long long>(groups, cap);
-#define QT_GO(NCHV, DEC, KCV, MCV)                                                              \
-    hipLaunchKernelGGL((gf_tile_kernel<kTileS, 8, NCHV, DEC, kTileD, KCV, MCV>), dim3(grid),     \
+#define QT_GO(NCHV, DEC, DV, KCV, MCV)                                                          \
+    hipLaunchKernelGGL((gf_tile_kernel<kTileS, 8, NCHV, DEC, DV, KCV, MCV>), dim3(grid),         \
                        dim3(threads), lds, st, in, out, coef, slots, nout, groups, k, m, rmax,  \
-                       coef_gstride, out_gstride)
+                       coef_gstride, out_gstride, t.tile_rot)
+#define QT_DEPTH(NCHV, DEC, KCV, MCV)                                                           \
+    do {                                                                                        \
+        if (t.tile_depth == 12) QT_GO(NCHV, DEC, 12, KCV, MCV);                                 \
+        else QT_GO(NCHV, DEC, 6, KCV, MCV);                                                     \
+    } while (0)
     if (decode) {
         note_kernel("gf_tile_kernel<decode>");
-        if (nch == 1) QT_GO(1, true, 0, 0);
-        else QT_GO(2, true, 0, 0);
-    } else if (t.tile_chunks == 3) {
-        // 15 waves (4 per SIMD but one): 3 chunks of 6 outputs
-        note_kernel("gf_tile_kernel<encode,k128m16,3x6>");
-        hipLaunchKernelGGL((gf_tile_kernel<kTileS, 6, 3, false, kTileD, 128, 16>), dim3(grid),
-                           dim3(TS::NT * 3 * 64), lds, st, in, out, coef, slots, nout, groups, k,
-                           m, rmax, coef_gstride, out_gstride);
+        if (nch == 1) QT_DEPTH(1, true, 0, 0);
+        else QT_DEPTH(2, true, 0, 0);
     } else {
         note_kernel("gf_tile_kernel<encode,k128m16>");
-        QT_GO(2, false, 128, 16);
+        QT_DEPTH(2, false, 128, 16);
     }
+#undef QT_DEPTH
 #undef QT_GO
     return hipGetLastError();
 }
