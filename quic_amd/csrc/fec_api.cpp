@@ -511,6 +511,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"dma", &t.dma, 0, 1},                 {"stream", &t.stream, 0, 1},
         {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
         {"const_enc", &t.const_enc, 0, 1},     {"tile", &t.tile, 0, 1},
+        {"stream_static", &t.stream_static, 0, 1},
         {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_depth", &t.tile_depth, 6, 12},
         {"tile_rot", &t.tile_rot, 0, 255},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
@@ -535,7 +536,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
     const std::pair<const char*, int> opts[] = {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
-        {"const_enc", t.const_enc}, {"tile", t.tile}, {"tile_grid", t.tile_grid},
+        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"tile", t.tile}, {"tile_grid", t.tile_grid},
         {"tile_depth", t.tile_depth}, {"tile_rot", t.tile_rot},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb},

@@ -23,6 +23,7 @@ struct Tune {
     int stream = 1;           // m > 1, small blocks: gf_stream (0: gf_apply)
     int stream_ring = 8;      // gf_stream: 1 KiB ring slots per wave (4..36), + 2 mirrored
     int stream_grid = 0;      // gf_stream: grid cap in workgroups (0: CUs x per-CU fit)
+    int stream_static = 1;    // gf_stream: compile-time ring schedule for k = 32, bb = 1352
     int const_enc = 1;        // encode kernels specialised for fixed (k, m) where compiled
     int tile = 1;             // m > 1, 9008-byte blocks: gf_tile (0: gf_apply)
     int tile_grid = 0;        // gf_tile: grid cap in workgroups (0: CUs x per-CU fit)

@@ -308,6 +308,224 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     stream_wait_vmcnt<0>();
 }
 
+// ------------------------------------------------------------------ static ring
+// gf_ring_kernel: the same stream for one FIXED shape (k = K blocks of 8 * S bytes: the
+// BASELINE B/C groups, (32 + 4) x 1352 B), with the whole per-group schedule known at
+// compile time.  A group is NP one-KiB pieces; piece n of a wave's stream lands in ring slot
+// (phase + n) mod R, phase = the group's first slot (advances by NP mod R per group).
+// Before block x's compute the ring holds every piece from block x's first one on and is
+// filled up to F(x) = pf(x) + R - 1 (the next group's first pieces included), so the number
+// of pieces per step, and the count of VMEM instructions younger than the next block's
+// last piece (plus the previous group's fixed-count stores where they sit in between), are
+// constants: every wait is an immediate `s_waitcnt vmcnt`, with no run-time bookkeeping.
+// The stream's ends are made regular too: the first group finds NST dummy stores (empty
+// buffer range) where a previous group's stores would be, and the last group issues
+// dummy pieces (a reread of its own last piece) for the group that does not follow.
+// No mirror: a block that wraps round the ring end (uniform test) is read with per-lane
+// wrapped addresses.
+constexpr int kRingWaves = 4;
+
+template <int S>
+struct RingShape {
+    static constexpr int R = 8, RB = R * 1024;
+    static constexpr int BB = 8 * S;
+    static constexpr int NW = (S + 3) / 4, NWF = S / 4;
+    static constexpr int SPR = 1 + ((S >> 1) & 1) + (S & 1);
+    static constexpr int pf(int x) { return (x * BB) >> 10; }             // first piece of block x
+    static constexpr int pl(int x) { return ((x + 1) * BB - 1) >> 10; }   // its last piece
+};
+
+template <int K, int S, int RC, bool DECODE, int MC>
+__global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
+    const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
+    const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
+    int rmax, long long coef_gstride, long long out_gstride) {
+    using SH = RingShape<S>;
+    constexpr int R = SH::R, RB = SH::RB, BB = SH::BB, NW = SH::NW, NWF = SH::NWF;
+    constexpr int GB = K * BB, NP = (GB + 1023) / 1024;
+    constexpr int NST = RC * 8 * SH::SPR;                 // stores per group, fixed
+    constexpr int RCP = RC < 4 ? 4 : RC, NCW = RCP / 4;
+    constexpr int SAUX = DECODE ? 0 : 2;                  // encode's parity stream: nt
+    constexpr int FM1 = SH::pf(K - 1) + R - 1 - NP;       // next-group pieces issued early
+    static_assert(!DECODE || MC == 0, "decode coefficients are per group");
+    static_assert(DECODE || MC == RC, "encode: one output per register set");
+    static_assert(FM1 >= SH::pl(0), "block 0 of the next group is prefetched in full");
+    static_assert(NP > R, "a group spans more than the ring");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63;
+    const int w = wave_id();
+    uint8_t* ring = smem + (size_t)w * RB;
+    const long long W = (long long)gridDim.x * kRingWaves;
+    const long long g0 = (long long)blockIdx.x * kRingWaves + w;
+    if (g0 >= groups) return;
+    const long long cnt = (groups - 1 - g0) / W + 1;      // groups of this wave
+    const int c = lane < NW ? lane : NW - 1;              // idle lanes shadow the last word
+    const long long gstep = W * GB;
+
+    const uint8_t* gsrc = in + g0 * GB;                   // current group's bytes
+    int phase = 0;                                        // ring slot of its piece 0
+    long long i = 0;                                      // current group
+
+    // piece n of the current group (n >= NP: piece n - NP of the next, or a dummy reread
+    // of the current group's last piece when there is no next group)
+    auto issue = [&](auto nc) __attribute__((always_inline)) {
+        constexpr int n = decltype(nc)::value;
+        const uint8_t* src;
+        int off;
+        if constexpr (n < NP) {
+            src = gsrc;
+            off = min(n * 1024 + lane * 16, GB - 16);
+        } else {
+            const bool next = i + 1 < cnt;
+            src = next ? gsrc + gstep : gsrc;
+            off = min((next ? n - NP : NP - 1) * 1024 + lane * 16, GB - 16);
+        }
+        const int slot = (phase + n) & (R - 1);
+        __builtin_amdgcn_global_load_lds(QS_GPTR(src + off), QS_LPTR(ring + slot * 1024), 16, 0,
+                                         2);
+    };
+    auto read_block = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8])
+                          __attribute__((always_inline)) {
+        constexpr int x = decltype(xc)::value;
+        uint32_t c4 = 4u * (uint32_t)c;
+        asm volatile("" : "+v"(c4));   // opaque: addresses are not hoisted across blocks
+        uint32_t bp = (uint32_t)phase * 1024u + (uint32_t)(x * BB);
+        bp = bp >= (uint32_t)RB ? bp - (uint32_t)RB : bp;   // phase * 1024 < RB, x*BB < ...
+        bp = bp >= (uint32_t)RB ? bp - (uint32_t)RB : bp;
+        bp = bp >= (uint32_t)RB ? bp - (uint32_t)RB : bp;
+        bp = bp >= (uint32_t)RB ? bp - (uint32_t)RB : bp;
+        bp = bp >= (uint32_t)RB ? bp - (uint32_t)RB : bp;
+        if (bp + (uint32_t)BB + 4u <= (uint32_t)RB) {
+            const uint8_t* L = ring + bp + c4;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int o = t * S;
+                const uint32_t* q = (const uint32_t*)(L + (o & ~3));
+                lo[t] = q[0];
+                hi[t] = (o & 3) ? q[1] : 0u;
+            }
+        } else {
+            const uint32_t base = bp + c4;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int o = t * S;
+                const uint32_t a0 = base + (uint32_t)(o & ~3);
+                lo[t] = *(const uint32_t*)(ring + min(a0, a0 - (uint32_t)RB));
+                if (o & 3) {
+                    const uint32_t a1 = a0 + 4u;
+                    hi[t] = *(const uint32_t*)(ring + min(a1, a1 - (uint32_t)RB));
+                } else {
+                    hi[t] = 0u;
+                }
+            }
+        }
+    };
+
+    // ---- prologue: the first group's early pieces, then the stores a previous group
+    // would have issued (dropped: empty range), so every group sees the same VMEM history
+    static_for<FM1 + 1>([&](auto nc) __attribute__((always_inline)) { issue(nc); });
+    {
+        const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0u, 0x00020000);
+#pragma unroll
+        for (int q = 0; q < NST; ++q) __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0u, 0, 0);
+    }
+
+    uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
+#pragma unroll 1
+    for (; i < cnt; ++i) {
+        const long long g = g0 + i * W;
+        int n = DECODE ? nout[g] : RC;
+        n = n > RC ? RC : n;
+        const uint32_t* cw = (const uint32_t*)(coef + (DECODE ? g * coef_gstride : 0));
+        uint32_t acc[RC][8];
+#pragma unroll
+        for (int j = 0; j < RC; ++j)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) acc[j][r] = 0;
+        // block 0: its pieces were issued before the previous group's stores
+        stream_wait_vmcnt<(FM1 - SH::pl(0) + NST > 63 ? 63 : FM1 - SH::pl(0) + NST)>();
+        read_block(std::integral_constant<int, 0>{}, lo0, hi0);
+
+        auto step = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
+                        uint32_t (&nhi)[8]) __attribute__((always_inline)) {
+            constexpr int x = decltype(xc)::value;
+            constexpr int F0 = x == 0 ? FM1 : SH::pf(x - 1) + R - 1;   // frontier before
+            constexpr int F1 = SH::pf(x) + R - 1;                       // and after this step
+            static_for<F1 - F0>([&](auto qc) __attribute__((always_inline)) {
+                issue(std::integral_constant<int, F0 + 1 + decltype(qc)::value>{});
+            });
+            if constexpr (x + 1 < K) {
+                constexpr int pl1 = SH::pl(x + 1);
+                constexpr int yng = F1 - pl1 + (pl1 <= FM1 ? NST : 0);
+                stream_wait_vmcnt<(yng > 63 ? 63 : yng)>();
+                read_block(std::integral_constant<int, x + 1>{}, nlo, nhi);
+            }
+            if (DECODE && n <= 0) return;   // no loss in this group: nothing to combine
+            WZ v;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int o = t * S;
+                v.W[t] = (o & 3) ? __builtin_amdgcn_alignbyte(hi[t], lo[t], o & 3) : lo[t];
+            }
+            if constexpr (!DECODE) {
+                Win win;
+                win_build(v.W8, win);
+                static_for<RC>([&](auto jc) __attribute__((always_inline)) {
+                    constexpr int j = decltype(jc)::value;
+                    win_apply<cauchy_coef_small(MC, j, x)>(acc[j], win);
+                });
+            } else {
+                uint32_t cwv[NCW];
+#pragma unroll
+                for (int q = 0; q < NCW; ++q) cwv[q] = cw[x * NCW + q];
+                expand_wz(v);
+#pragma unroll
+                for (int j = 0; j < RC; ++j) {
+                    if (j < n) {
+                        const uint32_t cf = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                        apply_nibble<0>(acc[j], cf & 15u, v);
+                        apply_nibble<4>(acc[j], cf >> 4, v);
+                    }
+                }
+            }
+        };
+        static_for<K>([&](auto xc) __attribute__((always_inline)) {
+#pragma unroll
+            for (int j = 0; j < RC; ++j)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
+            if constexpr (decltype(xc)::value % 2 == 0) step(xc, lo0, hi0, lo1, hi1);
+            else step(xc, lo1, hi1, lo0, hi0);
+        });
+
+        // ---- outputs: NST store instructions whatever n is (unused outputs: empty range)
+        uint32_t vo = lane < NWF ? 4u * (uint32_t)c : kSDrop;
+        uint32_t vt = lane == NWF && NWF < NW ? 4u * (uint32_t)c : kSDrop;
+        asm volatile("" : "+v"(vo), "+v"(vt));
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+            const bool on = j < n;
+            const int oslot = (DECODE && slots) ? (on ? sload_u8(slots, g * rmax + j) : 0) : j;
+            uint8_t* dst = out + g * out_gstride + (long long)oslot * BB;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(dst, 0, on ? (unsigned)BB : 0u, 0x00020000);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const uint32_t vsum = acc[j][r];
+                __builtin_amdgcn_raw_buffer_store_b32(vsum, rs, vo, r * S, SAUX);
+                if (S & 2)
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)vsum, rs, vt, r * S, SAUX);
+                if (S & 1)
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(vsum >> (8 * (S & 2))), rs, vt,
+                                                         r * S + (S & 2), SAUX);
+            }
+        }
+        gsrc += gstep;
+        phase = (phase + NP) & (R - 1);
+    }
+    stream_wait_vmcnt<0>();
+}
+
 bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& t) {
     (void)m;
     (void)decode;
@@ -359,6 +577,30 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         case 7: QS_GO(7, SV, false, 8, 0); break;         \
         case 8: QS_GO(8, SV, false, 8, 0); break;         \
         default: return hipErrorInvalidValue;             \
+    }
+    if (t.stream_static && k == 32 && s == 169 && (decode ? rc <= 4 : (m == 4 && t.const_enc))) {
+        // the fixed B/C shape: compile-time ring schedule (gf_ring_kernel)
+        const size_t rlds = (size_t)kRingWaves * RingShape<169>::RB;
+        const long long rwant = (groups + kRingWaves - 1) / kRingWaves;
+        long long rcap = (long long)t.cus * (int)((160 * 1024) / rlds);
+        if (t.stream_grid > 0) rcap = t.stream_grid;
+        const unsigned rgrid = (unsigned)std::min<long long>(rwant, rcap);
+#define QR_GO(RCV, DEC, MCV)                                                                   \
+    hipLaunchKernelGGL((gf_ring_kernel<32, 169, RCV, DEC, MCV>), dim3(rgrid),                   \
+                       dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax, \
+                       coef_gstride, out_gstride)
+        if (!decode) {
+            note_kernel("gf_ring_kernel<encode,k32m4>");
+            QR_GO(4, false, 4);
+        } else if (rc == 2) {
+            note_kernel("gf_ring_kernel<decode>");
+            QR_GO(2, true, 0);
+        } else {
+            note_kernel("gf_ring_kernel<decode>");
+            QR_GO(4, true, 0);
+        }
+#undef QR_GO
+        return hipGetLastError();
     }
     if (decode) {
         if (s == 169) {
