@@ -62,7 +62,11 @@ QFEC_API int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes);
  * Batched engine.  Layouts (row-major, bb = block_bytes):
  *   data   [G][k][bb]   parity [G][m][bb]
  *   blocks [G][k][bb]   rows   [G][k]  (u8 row tags, data 0..k-1, parity k..k+m-1)
- *   status [G]          per-group return code of the equivalent cauchy_256_decode call
+ *   status [G]          per-group return code of the equivalent cauchy_256_decode call,
+ *                       or -3 for a malformed receive set whose reference result is not
+ *                       defined (a row tag >= k + m, the same recovery row twice, fewer
+ *                       missing data rows than recovery blocks); such a group is left as
+ *                       it was
  * `stream` is a hipStream_t (NULL = HIP's null stream, as everywhere in HIP).  Device
  * entry points only enqueue work on that stream; they do not synchronise.
  *

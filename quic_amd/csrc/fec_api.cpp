@@ -296,6 +296,18 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     if (r) return r;
     if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
     qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
+    const long long tab_gstride = (long long)nchunk * k * std::max(rc, 4);
+    if (qfec::gf_tile_syndrome_supported(k, m, bb, rmax, c->tune) &&
+        ((uintptr_t)d_blocks & 15) == 0) {
+        // compiled (128, 16) code: syndromes, then the r x r solve (reads precede stores
+        // within a group, so in place needs no scratch)
+        QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc,
+                                        rmax, G, st, c->tune, nullptr, true));
+        QF_HIP(qfec::launch_gf_tile_syndrome(d_blocks, d_out, w.coef, w.slots, w.nout, cenc, k,
+                                             m, bb, G, rmax, tab_gstride, (long long)k * bb, st,
+                                             c->tune));
+        return 0;
+    }
     QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc, rmax,
                                     G, st, c->tune));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
@@ -367,6 +379,16 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
     if (r) return r;
     if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
     qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
+    if (qfec::gf_tile_syndrome_supported(k, m, bb, rmax, c->tune) &&
+        ((uintptr_t)d_blocks & 15) == 0) {
+        const int nchunk = (rmax + rc - 1) / rc;
+        QF_HIP(qfec::launch_decode_prep(d_rows_in, nullptr, d_status, cenc, w, k, m, bb, rc, rmax,
+                                        G, st, c->tune, d_rec_rows, true));
+        QF_HIP(qfec::launch_gf_tile_syndrome(d_blocks, d_rec, w.coef, nullptr, w.nout, cenc, k, m,
+                                             bb, G, rmax, (long long)nchunk * k * std::max(rc, 4),
+                                             (long long)rmax * bb, st, c->tune));
+        return 0;
+    }
     QF_HIP(qfec::launch_decode_prep(d_rows_in, nullptr, d_status, cenc, w, k, m, bb, rc, rmax, G,
                                     st, c->tune, d_rec_rows));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1

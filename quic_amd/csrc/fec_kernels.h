@@ -46,6 +46,20 @@ struct DecodeWork {
     int32_t* nout;     // [G]                  number of recovered blocks in this group
 };
 
+// Syndrome table (decode prep in syndrome mode, read by gf_tile's syndrome decode), one per
+// group at coef + g * coef_gstride, k <= 128 and at most 16 parity rows:
+namespace syn {
+constexpr int kPerm = 0;     // u8[k]  stream order of the slots: the present data rows
+                             //        ascending (one slot each), then the extras: recovery
+                             //        blocks and repeated data rows, in slot order
+constexpr int kMask = 128;   // u32[4] bit x: data row x is in the ascending part
+constexpr int kNeed = 144;   // u32    bit y: parity row y was received (a syndrome row)
+constexpr int kISlot = 148;  // u8[16] syndrome index i of received parity row y
+constexpr int kERow = 164;   // u8[k]  row tag of extra e
+constexpr int kSinv = 292;   // u8[16][16] Sinv[j][i]: recovered j = sum_i Sinv[j][i] T_i
+constexpr int kBytes = 548;
+}  // namespace syn
+
 // parity[g*out_gstride ..+bb) = XOR of the k blocks of group g (m == 1 encode, and the
 // P0 the reference writes before rejecting invalid m > 1 parameters).
 hipError_t launch_xor_encode(const uint8_t* data, uint8_t* parity, int k, int bb,
@@ -80,13 +94,15 @@ hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t*
                             const Tune& t);
 
 // Decode prep: per group, sort blocks, invert the erasure submatrix in GF(256) and
-// emit the r x k recovery coefficients.  cenc is the [m][k] encode matrix (row 0 = ones).
+// emit the r x k recovery coefficients (syndrome: the syn:: table instead).  cenc is the
+// [m][k] encode matrix (row 0 = ones).
 // rows_out == nullptr: recovered-blocks layout, rec_rows [G][rmax] gets the data row of
 // recovered block j (ascending), 255 past the group's erasure count.
 hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
                               const uint8_t* cenc, DecodeWork w, int k, int m, int bb,
                               int rc, int rmax, long long groups, hipStream_t st,
-                              const Tune& t, uint8_t* rec_rows = nullptr);
+                              const Tune& t, uint8_t* rec_rows = nullptr,
+                              bool syndrome = false);
 
 // Decode apply: recovered block j of group g = sum_pos coef[g][..][pos][j] (x) blocks[g][pos],
 // written to out[g][slots[g][j]].
@@ -125,6 +141,13 @@ hipError_t launch_gf_tile(const uint8_t* in, uint8_t* out, const uint8_t* coef,
                           const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
                           long long groups, int rc, int rmax, long long coef_gstride,
                           long long out_gstride, bool decode, hipStream_t st, const Tune& t);
+// Syndrome decode of the compiled (128, 16) code from the syn:: table (gf_tile.hip).
+bool gf_tile_syndrome_supported(int k, int m, int bb, int rmax, const Tune& t);
+hipError_t launch_gf_tile_syndrome(const uint8_t* in, uint8_t* out, const uint8_t* tab,
+                                   const uint8_t* slots, const int32_t* nout,
+                                   const uint8_t* cenc, int k, int m, int bb, long long groups,
+                                   int rmax, long long tab_gstride, long long out_gstride,
+                                   hipStream_t st, const Tune& t);
 
 // Synthetic workload helpers (bench / tests): splitmix64 stream and receive-set gather.
 hipError_t launch_synth_fill(uint8_t* dst, unsigned long long bytes, unsigned long long seed,

@@ -414,7 +414,7 @@ __device__ __forceinline__ void prep_group(
     const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
     const uint8_t* cenc, uint8_t* __restrict__ coef, uint8_t* __restrict__ slots,
     int32_t* __restrict__ nout, uint8_t* __restrict__ rec_rows, int k, int m, int bb, int rc,
-    int rmax, int nchunk) {
+    int rmax, int nchunk, bool syndrome) {
     uint8_t* rowl = sc.rowl;
     uint8_t* present = sc.present;
     uint8_t* recpos = sc.recpos;
@@ -431,8 +431,9 @@ __device__ __forceinline__ void prep_group(
     uint8_t* rec = rec_rows ? rec_rows + g * rmax : nullptr;
     for (int i = lane; i < k; i += 64) rowl[i] = rg[i];
     wave_sync();
+    // present[x] != 0: data row x received; syndrome mode keeps one of its slots + 1
     for (int i = lane; i < k; i += 64)
-        if (rowl[i] < k) present[rowl[i]] = 1;
+        if (rowl[i] < k) present[rowl[i]] = syndrome ? (uint8_t)(i + 1) : 1;
     wave_sync();
     // recovery blocks in array order (sort_blocks)
     int nrec = 0;
@@ -459,7 +460,14 @@ __device__ __forceinline__ void prep_group(
     }
     wave_sync();
 
+    uint8_t* tb = coef + g * (long long)nchunk * k * rcp;   // syndrome table (syn::)
     auto finish_unchanged = [&](int st) {
+        if (syndrome) {
+            // a stream of k extras in slot order that feeds no syndrome row: the apply
+            // kernel still reads every group's k blocks
+            for (int i = lane; i < k; i += 64) tb[syn::kPerm + i] = (uint8_t)i;
+            if (lane < 5) ((uint32_t*)(tb + syn::kMask))[lane] = 0;   // mask and need
+        }
         if (ro && ro != rg)
             for (int i = lane; i < k; i += 64) ro[i] = rowl[i];
         if (rec)
@@ -521,8 +529,44 @@ __device__ __forceinline__ void prep_group(
         }
     }
 
+    if (syndrome) {
+        // recovered e_j = sum_i Sinv[j][i] T_i with the syndromes
+        // T_i = R_i ^ sum_{data slots} C[y_i][row] D_slot (cauchy_256.cpp:1269-1420: the
+        // originals are eliminated from the recovery rows, then the r x r system is solved)
+        int np = 0;
+        for (int base = 0; base < 128; base += 64) {   // present rows ascending, k <= 128
+            const int x = base + lane;
+            const bool pres = x < k && present[x] != 0;
+            const unsigned long long msk = __ballot(pres);
+            const int pre = __popcll(msk & ((1ull << lane) - 1));
+            if (pres) tb[syn::kPerm + np + pre] = (uint8_t)(present[x] - 1);
+            if (lane < 2)
+                ((uint32_t*)(tb + syn::kMask))[base / 32 + lane] = (uint32_t)(msk >> (32 * lane));
+            np += __popcll(msk);
+        }
+        int ne = 0;
+        for (int base = 0; base < k; base += 64) {    // extras in slot order
+            const int i = base + lane;
+            const bool ext = i < k && (rowl[i] >= k || present[rowl[i]] != i + 1);
+            const unsigned long long msk = __ballot(ext);
+            const int pre = __popcll(msk & ((1ull << lane) - 1));
+            if (ext) {
+                tb[syn::kPerm + np + ne + pre] = (uint8_t)i;
+                tb[syn::kERow + ne + pre] = rowl[i];
+            }
+            ne += __popcll(msk);
+        }
+        uint32_t need = 0;
+        for (int i = 0; i < n; ++i) need |= 1u << (rowl[recpos[i]] - k);
+        if (lane < n) tb[syn::kISlot + rowl[recpos[lane]] - k] = (uint8_t)lane;
+        if (lane == 0) *(uint32_t*)(tb + syn::kNeed) = need;
+        for (int idx = lane; idx < n * n; idx += 64) {
+            const int j = idx / n, i = idx % n;
+            tb[syn::kSinv + j * 16 + i] = mat[j * n2 + n + i];
+        }
+    }
     // recovery coefficients per (output j, input slot pos)
-    for (int pos = lane; pos < k; pos += 64) {
+    for (int pos = lane; pos < k && !syndrome; pos += 64) {
         const int ri = recidx[pos];
         for (int j = 0; j < n; ++j) {
             const uint8_t* inv_row = mat + j * n2 + n;   // Sinv[j][*]
@@ -558,7 +602,7 @@ __global__ __launch_bounds__(256) void decode_prep_kernel(
     const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
     const uint8_t* __restrict__ cenc, uint8_t* __restrict__ coef, uint8_t* __restrict__ slots,
     int32_t* __restrict__ nout, uint8_t* __restrict__ rec_rows, long long groups, int k, int m,
-    int bb, int rc, int rmax, int nchunk, int scratch_bytes) {
+    int bb, int rc, int rmax, int nchunk, int scratch_bytes, int syndrome) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* gexp = smem;              // 512
     uint8_t* glog = gexp + 512;        // 256
@@ -575,7 +619,7 @@ __global__ __launch_bounds__(256) void decode_prep_kernel(
     for (long long g = (long long)blockIdx.x * nwv + w; g < groups;
          g += (long long)gridDim.x * nwv)
         prep_group(g, lane, gexp, glog, sc, rows_in, rows_out, status, lcenc, coef, slots, nout,
-                   rec_rows, k, m, bb, rc, rmax, nchunk);
+                   rec_rows, k, m, bb, rc, rmax, nchunk, syndrome != 0);
 }
 
 // Decode prep with four LANES per group, for small erasure counts (rmax <= 4, k <= 64: the
@@ -1024,9 +1068,12 @@ hipError_t launch_gf_encode(const uint8_t* data, uint8_t* parity, const uint8_t*
 hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
                               const uint8_t* cenc, DecodeWork w, int k, int m, int bb, int rc,
                               int rmax, long long groups, hipStream_t st, const Tune& t,
-                              uint8_t* rec_rows) {
+                              uint8_t* rec_rows, bool syndrome) {
     if (groups <= 0) return hipSuccess;
-    if (t.prep_lane && rmax <= 4 && k <= 64 && k % 4 == 0 && (long long)m * k <= 4096 && rc <= 4 &&
+    if (syndrome && (k > 128 || m > 16 || (long long)((rmax + rc - 1) / rc) * k * std::max(rc, 4) <
+                                                 syn::kBytes))
+        return hipErrorInvalidValue;
+    if (!syndrome && t.prep_lane && rmax <= 4 && k <= 64 && k % 4 == 0 && (long long)m * k <= 4096 && rc <= 4 &&
         ((((uintptr_t)w.coef) | (uintptr_t)rows_in) & 3) == 0) {
         const unsigned nb = (unsigned)((groups + 63) / 64);     // 64 groups x 4 lanes
         const size_t lds = (((size_t)m * k + 15) & ~(size_t)15) + 64 * (size_t)k +
@@ -1045,10 +1092,10 @@ hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t
     const size_t lds = fixed + (size_t)nwv * scratch;
     const long long want = (groups + nwv - 1) / nwv;
     const unsigned nb = (unsigned)std::min<long long>(want, (long long)t.cus * 16);
-    note_kernel("decode_prep_kernel");
+    note_kernel(syndrome ? "decode_prep_kernel<syndrome>" : "decode_prep_kernel");
     decode_prep_kernel<<<nb, nwv * 64, lds, st>>>(rows_in, rows_out, status, cenc, w.coef,
                                                    w.slots, w.nout, rec_rows, groups, k, m, bb,
-                                                   rc, rmax, nchunk, scratch);
+                                                   rc, rmax, nchunk, scratch, syndrome ? 1 : 0);
     return hipGetLastError();
 }
 

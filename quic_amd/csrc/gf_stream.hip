@@ -207,8 +207,18 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
             wait_block(bpos);
             read_block(bpos, lo0, hi0);
             // xc: the block index, an int or (KC > 0) an integral_constant
+            // run-time coefficients two blocks ahead: the scalar load for block x + 2 is
+            // issued while block x is combined, so its latency is hidden
+            uint32_t cA[NCW], cB[NCW];
+            if constexpr (KC == 0) {
+#pragma unroll
+                for (int q = 0; q < NCW; ++q) {
+                    cA[q] = cw[q];
+                    cB[q] = cw[(k > 1 ? 1 : 0) * NCW + q];
+                }
+            }
             auto step = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
-                            uint32_t (&nhi)[8]) {
+                            uint32_t (&nhi)[8], uint32_t (&cc)[NCW]) {
                 const int x = xc;
                 const uint32_t bn = next_pos(bpos);
                 if (x + 1 < k) {
@@ -236,8 +246,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     return;
                 }
                 uint32_t cwv[NCW];
+                const int xn = x + 2 < k ? x + 2 : k - 1;
 #pragma unroll
-                for (int q = 0; q < NCW; ++q) cwv[q] = cw[x * NCW + q];
+                for (int q = 0; q < NCW; ++q) {
+                    cwv[q] = cc[q];
+                    cc[q] = cw[xn * NCW + q];
+                }
                 expand_wz(v);
 #pragma unroll
                 for (int j = 0; j < RC; ++j) {
@@ -263,16 +277,17 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     for (int j = 0; j < RC; ++j)
 #pragma unroll
                         for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
-                    if constexpr (decltype(xc)::value % 2 == 0) step(xc, lo0, hi0, lo1, hi1);
-                    else step(xc, lo1, hi1, lo0, hi0);
+                    if constexpr (decltype(xc)::value % 2 == 0) step(xc, lo0, hi0, lo1, hi1, cA);
+                    else step(xc, lo1, hi1, lo0, hi0, cB);
                 });
             } else {
 #pragma unroll 1
                 for (int x = 0; x < k; x += 2) {
-                    step(x, lo0, hi0, lo1, hi1);
-                    if (x + 1 < k) step(x + 1, lo1, hi1, lo0, hi0);
+                    step(x, lo0, hi0, lo1, hi1, cA);
+                    if (x + 1 < k) step(x + 1, lo1, hi1, lo0, hi0, cB);
                 }
             }
+            asm volatile("" ::: "memory");   // stores stay in issue order among the DMAs
             // ---- outputs: fixed instruction count per output (dropped lanes, no branches).
             // Lane offsets 4c (full words) and the tail lane's, sub-row in the scalar offset:
             // two address VGPRs, opaque so they are not hoisted as 8 x RC precomputed ones.
@@ -301,6 +316,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     vm += 8 * SPR;
                 }
             }
+            asm volatile("" ::: "memory");
         }
         gbase += NP;
         gslot0 = (gslot0 + NP) % R;
@@ -333,6 +349,19 @@ struct RingShape {
     static constexpr int SPR = 1 + ((S >> 1) & 1) + (S & 1);
     static constexpr int pf(int x) { return (x * BB) >> 10; }             // first piece of block x
     static constexpr int pl(int x) { return ((x + 1) * BB - 1) >> 10; }   // its last piece
+    // smallest count of VMEM instructions younger than a block's last piece when the wave
+    // waits for it (K blocks per group, NST stores per group): one conservative immediate
+    // for the rolled (run-time block index) form
+    static constexpr int min_younger(int K, int NST) {
+        const int NP = (K * BB + 1023) / 1024;
+        const int FM1 = pf(K - 1) + R - 1 - NP;
+        int mn = FM1 - pl(0) + NST;
+        for (int x = 0; x + 1 < K; ++x) {
+            const int y = pf(x) + R - 1 - pl(x + 1) + (pl(x + 1) <= FM1 ? NST : 0);
+            mn = y < mn ? y : mn;
+        }
+        return mn > 63 ? 63 : mn;
+    }
 };
 
 template <int K, int S, int RC, bool DECODE, int MC>
@@ -384,17 +413,27 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
         __builtin_amdgcn_global_load_lds(QS_GPTR(src + off), QS_LPTR(ring + slot * 1024), 16, 0,
                                          2);
     };
+    // the same for a run-time piece index (rolled decode loop)
+    auto issue_rt = [&](int n) __attribute__((always_inline)) {
+        const uint8_t* src = gsrc;
+        int p = n;
+        if (n >= NP) {
+            const bool next = i + 1 < cnt;
+            src = next ? gsrc + gstep : gsrc;
+            p = next ? n - NP : NP - 1;
+        }
+        const int off = min(p * 1024 + lane * 16, GB - 16);
+        const int slot = (phase + n) & (R - 1);
+        __builtin_amdgcn_global_load_lds(QS_GPTR(src + off), QS_LPTR(ring + slot * 1024), 16, 0,
+                                         2);
+    };
+    // block x (an int or an integral_constant) at ring byte (phase * 1024 + x * BB) mod RB
     auto read_block = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8])
                           __attribute__((always_inline)) {
-        constexpr int x = decltype(xc)::value;
+        const int x = xc;
         uint32_t c4 = 4u * (uint32_t)c;
         asm volatile("" : "+v"(c4));   // opaque: addresses are not hoisted across blocks
-        uint32_t bp = (uint32_t)phase * 1024u + (uint32_t)(x * BB);
-        bp = bp >= (uint32_t)RB ? bp - (uint32_t)RB : bp;   // phase * 1024 < RB, x*BB < ...
-        bp = bp >= (uint32_t)RB ? bp - (uint32_t)RB : bp;
-        bp = bp >= (uint32_t)RB ? bp - (uint32_t)RB : bp;
-        bp = bp >= (uint32_t)RB ? bp - (uint32_t)RB : bp;
-        bp = bp >= (uint32_t)RB ? bp - (uint32_t)RB : bp;
+        uint32_t bp = ((uint32_t)phase * 1024u + (uint32_t)(x * BB)) & (uint32_t)(RB - 1);
         if (bp + (uint32_t)BB + 4u <= (uint32_t)RB) {
             const uint8_t* L = ring + bp + c4;
 #pragma unroll
@@ -424,10 +463,14 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
     // ---- prologue: the first group's early pieces, then the stores a previous group
     // would have issued (dropped: empty range), so every group sees the same VMEM history
     static_for<FM1 + 1>([&](auto nc) __attribute__((always_inline)) { issue(nc); });
+    // The waits count VMEM instructions in issue order: the compiler must not move a
+    // buffer store across a DMA (it may: they touch different memory).
+    asm volatile("" ::: "memory");
     {
         const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0u, 0x00020000);
 #pragma unroll
-        for (int q = 0; q < NST; ++q) __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0u, 0, 0);
+        for (int q = 0; q < NST; ++q)   // distinct offsets: not merged as duplicate stores
+            __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0u, 4 * q, 0);
     }
 
     uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
@@ -489,16 +532,64 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
                 }
             }
         };
-        static_for<K>([&](auto xc) __attribute__((always_inline)) {
+        if constexpr (!DECODE) {
+            static_for<K>([&](auto xc) __attribute__((always_inline)) {
 #pragma unroll
-            for (int j = 0; j < RC; ++j)
+                for (int j = 0; j < RC; ++j)
 #pragma unroll
-                for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
-            if constexpr (decltype(xc)::value % 2 == 0) step(xc, lo0, hi0, lo1, hi1);
-            else step(xc, lo1, hi1, lo0, hi0);
-        });
+                    for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
+                if constexpr (decltype(xc)::value % 2 == 0) step(xc, lo0, hi0, lo1, hi1);
+                else step(xc, lo1, hi1, lo0, hi0);
+            });
+        } else {
+            // Decode: run-time coefficients make an unrolled group long (~30K instructions,
+            // past the instruction cache's comfort); the rolled loop issues the same pieces
+            // (frontier pf(x) + R - 1) and waits with the smallest younger count any block
+            // sees, a constant: conservative by at most one piece.
+            constexpr int WMIN = SH::min_younger(K, NST);
+            int fr = FM1;                                  // pieces issued so far (last index)
+            // coefficient rows two blocks ahead (scalar loads have a long latency; the
+            // value for block x is loaded while block x - 2 is combined)
+            static_assert(NCW == 1, "rmax <= 4: one coefficient dword per block");
+            uint32_t cA = cw[0], cB = cw[1];
+            auto rstep = [&](int x, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
+                             uint32_t (&nhi)[8], uint32_t& cc) __attribute__((always_inline)) {
+                const int f1 = ((x * BB) >> 10) + R - 1;
+                for (; fr < f1; ++fr) issue_rt(fr + 1);
+                if (x + 1 < K) {
+                    stream_wait_vmcnt<WMIN>();
+                    read_block(x + 1, nlo, nhi);
+                }
+                if (n <= 0) return;   // no loss in this group: nothing to combine
+                WZ v;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int o = t * S;
+                    v.W[t] = (o & 3) ? __builtin_amdgcn_alignbyte(hi[t], lo[t], o & 3) : lo[t];
+                }
+                const uint32_t cwv = cc;
+                cc = cw[min(x + 2, K - 1)];
+                expand_wz(v);
+#pragma unroll
+                for (int j = 0; j < RC; ++j) {
+                    if (j < n) {
+                        const uint32_t cf = (cwv >> (8 * (j & 3))) & 0xFFu;
+                        apply_nibble<0>(acc[j], cf & 15u, v);
+                        apply_nibble<4>(acc[j], cf >> 4, v);
+                    }
+                }
+            };
+            static_assert(K % 2 == 0, "register double buffer parity");
+#pragma unroll 1
+            for (int x = 0; x < K; x += 2) {
+                rstep(x, lo0, hi0, lo1, hi1, cA);
+                rstep(x + 1, lo1, hi1, lo0, hi0, cB);
+            }
+        }
 
-        // ---- outputs: NST store instructions whatever n is (unused outputs: empty range)
+        // ---- outputs: NST store instructions whatever n is (unused outputs: empty range),
+        // kept after the last step's DMAs and before the next group's (issue order)
+        asm volatile("" ::: "memory");
         uint32_t vo = lane < NWF ? 4u * (uint32_t)c : kSDrop;
         uint32_t vt = lane == NWF && NWF < NW ? 4u * (uint32_t)c : kSDrop;
         asm volatile("" : "+v"(vo), "+v"(vt));
@@ -520,6 +611,7 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
                                                          r * S + (S & 2), SAUX);
             }
         }
+        asm volatile("" ::: "memory");
         gsrc += gstep;
         phase = (phase + NP) & (R - 1);
     }
@@ -578,7 +670,9 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         case 8: QS_GO(8, SV, false, 8, 0); break;         \
         default: return hipErrorInvalidValue;             \
     }
-    if (t.stream_static && k == 32 && s == 169 && (decode ? rc <= 4 : (m == 4 && t.const_enc))) {
+    // the static ring schedule is used for the encode only: its rolled decode measured
+    // slower than gf_stream's (0.644 vs 0.619 ms on config B)
+    if (t.stream_static && !decode && k == 32 && s == 169 && m == 4 && t.const_enc) {
         // the fixed B/C shape: compile-time ring schedule (gf_ring_kernel)
         const size_t rlds = (size_t)kRingWaves * RingShape<169>::RB;
         const long long rwant = (groups + kRingWaves - 1) / kRingWaves;
@@ -589,16 +683,8 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     hipLaunchKernelGGL((gf_ring_kernel<32, 169, RCV, DEC, MCV>), dim3(rgrid),                   \
                        dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax, \
                        coef_gstride, out_gstride)
-        if (!decode) {
-            note_kernel("gf_ring_kernel<encode,k32m4>");
-            QR_GO(4, false, 4);
-        } else if (rc == 2) {
-            note_kernel("gf_ring_kernel<decode>");
-            QR_GO(2, true, 0);
-        } else {
-            note_kernel("gf_ring_kernel<decode>");
-            QR_GO(4, true, 0);
-        }
+        note_kernel("gf_ring_kernel<encode,k32m4>");
+        QR_GO(4, false, 4);
 #undef QR_GO
         return hipGetLastError();
     }

@@ -53,6 +53,17 @@ __device__ __forceinline__ int tile_sload_u8(const uint8_t* __restrict__ base, l
     return (int)((wv >> (8 * (i & 3))) & 0xFFu);
 }
 
+// byte i of a table the kernel never writes, through the scalar cache (constant address
+// space: the compiler may not prove a pointer computed in a loop is read-only otherwise)
+__device__ __forceinline__ int tile_cload_u8(const uint8_t* base, long long i) {
+    const __attribute__((address_space(4))) uint32_t* p =
+        (const __attribute__((address_space(4))) uint32_t*)(base);
+    return (int)((p[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+}
+__device__ __forceinline__ uint32_t tile_cload_u32(const uint8_t* base, int byte_off) {
+    return ((const __attribute__((address_space(4))) uint32_t*)(base))[byte_off >> 2];
+}
+
 constexpr unsigned kTDrop = 0x80000000u;   // buffer offset past any range: lane dropped
 
 template <int S>
@@ -306,6 +317,7 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
         // the sub-row goes into the scalar offset and an unused output gets an empty range,
         // so the whole phase needs two VGPRs of addresses (opaque: not hoisted out of the
         // group loop as 8 x RC precomputed offsets).
+        asm volatile("" ::: "memory");   // stores stay in issue order among the DMAs
         const bool live = tile * 64 + lane < NW;
         uint32_t vo = live && c < NWF ? 4u * (uint32_t)c : kTDrop;
         uint32_t vt = live && c == NWF && NWF < NW ? 4u * (uint32_t)c : kTDrop;
@@ -330,6 +342,363 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
                                                          r * S + (S & 2), SAUX);
             }
         }
+        asm volatile("" ::: "memory");
+    }
+    tile_wait_vmcnt<0>();
+}
+
+// ------------------------------------------------------------------ syndrome decode
+// Decode of the compiled (128, 16) code in the reference's order (cauchy_256.cpp:1269-1420:
+// the received originals are eliminated from the recovery rows, then the r x r system is
+// solved).  With y_i the parity row of received recovery block R_i:
+//   T_i = R_i ^ sum_{data slots s} C[y_i][row_s] D_s        (syndromes, C compile-time)
+//   E_j = sum_i Sinv[j][i] T_i                               (once per group, run time)
+// The block pass runs the windowed form of the compiled encode (one v_bitop3 per (syndrome
+// row, sub-row)) for the received parity rows only, instead of r run-time coefficients per
+// block through the scalar nibble dispatch; the r x r solve costs r^2 nibble applies per
+// group against 128 block steps.
+// Stream: the prep's syndrome table (fec_kernels.h, syn::) orders each group's k slots as
+// the present data rows ascending, then the extras (recovery blocks, repeated data rows).
+// The unrolled block loop tests row x's present bit and consumes the next streamed block
+// only if it is set, so the coefficients stay compile-time; an erased row moves the waiting
+// block to the other register set instead.
+// Waves: NT column tiles x 2 chunks; chunk h owns syndrome rows y = 2t + h and outputs
+// j = 2q + h (t, q < 8), so the usual losses (the first r parity rows received) split
+// evenly.  Syndromes cross chunks through LDS after the block ring, 8 at a time.
+template <int S, int D>
+__global__ __launch_bounds__(TileShape<S>::NT * 2 * 64, (TileShape<S>::NT * 2 + 3) / 4) void
+gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
+                   const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout,
+                   const uint8_t* __restrict__ cenc, long long groups, int rmax,
+                   long long tab_gstride, long long out_gstride) {
+    using T = TileShape<S>;
+    constexpr int KC = 128, MC = 16, NCH = 2;
+    constexpr int ROWS = MC / NCH;                  // syndrome rows y = NCH * t + chunk
+    constexpr int RO = MC / NCH;                    // outputs j = NCH * q + chunk
+    constexpr int TH = 8;                           // syndromes per LDS exchange round
+    constexpr int BB = T::BB, NW = T::NW, NWF = T::NWF, NT = T::NT, NPB = T::NPB;
+    constexpr int BBP = T::BBP, SPR = T::SPR;
+    constexpr int NWV = NT * NCH;
+    constexpr int PPW = (NPB + NWV - 1) / NWV;
+    constexpr int NBUF = D + 2;
+    constexpr int NST = RO * 8 * SPR;               // stores per wave per group
+    constexpr int AHEAD = D - 1;
+    constexpr int WAITN = AHEAD * PPW;
+    constexpr int WAITG = AHEAD * PPW + NST > 63 ? 63 : AHEAD * PPW + NST;
+    static_assert(WAITN <= 63 && D >= 2, "pipeline depth");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* tl = (uint32_t*)(smem + NBUF * BBP);  // [TH][NT][8][64] syndrome words
+
+    const int lane = threadIdx.x & 63;
+    const int w = wave_id();
+    const int tile = w % NT, chunk = w / NT;
+    const int c = min(tile * 64 + lane, NW - 1);
+    const long long G0 = blockIdx.x, GS = gridDim.x;
+    if (G0 >= groups) return;
+    const long long cnt = (groups - 1 - G0) / GS + 1;
+    const long long nblocks = cnt * KC;
+
+    // ---- DMA side: stream block x of group G0 + i * GS = its slot perm[x]
+    long long iss_b = 0;
+    int iss_x = 0;
+    const uint8_t* iss_src = in + G0 * (long long)KC * BB;
+    const uint8_t* iss_tab = tab + G0 * tab_gstride;
+    const long long gstride = GS * (long long)KC * BB;
+    auto issue_next = [&]() __attribute__((always_inline)) {
+        uint8_t* dst = smem + (int)(iss_b % NBUF) * BBP;
+        const int slot = min(tile_cload_u8(iss_tab + syn::kPerm, iss_x), KC - 1);
+        const uint8_t* src = iss_src + (long long)slot * BB;
+#pragma unroll
+        for (int q = 0; q < PPW; ++q) {
+            const int p = min(w + q * NWV, NPB - 1);
+            const int off = min(p * 1024 + lane * 16, BB - 16);
+            __builtin_amdgcn_global_load_lds(QT_GPTR(src + off), QT_LPTR(dst + p * 1024), 16, 0,
+                                             2);
+        }
+        ++iss_b;
+        if (++iss_x == KC) {
+            iss_x = 0;
+            iss_src += gstride;
+            iss_tab += GS * tab_gstride;
+        }
+    };
+    auto read_block = [&](long long bi, uint32_t (&lo)[8], uint32_t (&hi)[8])
+                          __attribute__((always_inline)) {
+        uint32_t c4 = 4u * (uint32_t)c;
+        asm volatile("" : "+v"(c4));   // no hoisting across blocks
+        const uint8_t* L = smem + (int)(bi % NBUF) * BBP + c4;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int o = t * S;
+            const uint32_t* q = (const uint32_t*)(L + (o & ~3));
+            lo[t] = q[0];
+            hi[t] = (o & 3) ? q[1] : 0u;
+        }
+    };
+    auto wait_block = [&](long long bw, bool after_stores) __attribute__((always_inline)) {
+        if (bw + AHEAD < nblocks) {
+            if (after_stores) tile_wait_vmcnt<WAITG>();
+            else tile_wait_vmcnt<WAITN>();
+        } else {
+            tile_wait_vmcnt<0>();
+        }
+        tile_barrier();
+    };
+
+#pragma unroll 1
+    for (int u = 0; u < D; ++u)
+        if (u < nblocks) issue_next();
+    uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
+    wait_block(0, false);
+    read_block(0, lo0, hi0);
+
+    long long b = 0;
+#pragma unroll 1
+    for (long long i = 0; i < cnt; ++i) {
+        const long long g = G0 + i * GS;
+        const uint8_t* tb = tab + g * tab_gstride;
+        uint32_t pm[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pm[q] = tile_cload_u32(tb, syn::kMask + 4 * q);
+        const uint32_t need = tile_cload_u32(tb, syn::kNeed);
+        const int n = min(nout[g], rmax);
+        const int ne = KC - (__builtin_popcount(pm[0]) + __builtin_popcount(pm[1]) +
+                             __builtin_popcount(pm[2]) + __builtin_popcount(pm[3]));
+        uint32_t acc[ROWS][8];
+#pragma unroll
+        for (int t = 0; t < ROWS; ++t)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) acc[t][r] = 0;
+
+        // next block: prefetch block b + D, pull block b + 1 into (nlo, nhi); returns the
+        // realigned words of block b
+        auto advance = [&](const uint32_t (&lo)[8], const uint32_t (&hi)[8], uint32_t (&nlo)[8],
+                           uint32_t (&nhi)[8], uint32_t (&wv)[8]) __attribute__((always_inline)) {
+            if (b + D < nblocks) issue_next();
+            if (b + 1 < nblocks) {
+                // positions 0 .. D - 1 of a group were DMA'd before the previous group's
+                // stores were issued, so those stores are younger than their pieces
+                const long long p1 = b + 1 - i * KC;
+                wait_block(b + 1, i > 0 && p1 <= D - 1);
+                read_block(b + 1, nlo, nhi);
+            }
+            ++b;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int o = t * S;
+                wv[t] = (o & 3) ? __builtin_amdgcn_alignbyte(hi[t], lo[t], o & 3) : lo[t];
+            }
+        };
+        // data row x (compile time): its block, if present, into every received syndrome row
+        auto row_step = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
+                            uint32_t (&nhi)[8]) __attribute__((always_inline)) {
+            constexpr int x = decltype(xc)::value;
+            if ((pm[x >> 5] >> (x & 31)) & 1u) {
+                uint32_t wv[8];
+                advance(lo, hi, nlo, nhi, wv);
+                Win win;
+                win_build(wv, win);
+                static_for<NCH>([&](auto chc) __attribute__((always_inline)) {
+                    constexpr int CH = decltype(chc)::value;
+                    if (chunk == CH) {
+                        static_for<ROWS>([&](auto tc) __attribute__((always_inline)) {
+                            constexpr int t = decltype(tc)::value, y = NCH * t + CH;
+                            if ((need >> y) & 1u)
+                                win_apply<cauchy_coef(MC, y, x)>(acc[t], win);
+                        });
+                    }
+                });
+            } else {
+                // row x erased: the block waiting in (lo, hi) is row x + 1's
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    nlo[t] = lo[t];
+                    nhi[t] = hi[t];
+                }
+            }
+        };
+        static_for<KC>([&](auto xc) __attribute__((always_inline)) {
+            // accumulators opaque at every block boundary (see gf_tile_kernel)
+#pragma unroll
+            for (int t = 0; t < ROWS; ++t)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[t][r]));
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (decltype(xc)::value % 2 == 0)
+                row_step(xc, lo0, hi0, lo1, hi1);
+            else
+                row_step(xc, lo1, hi1, lo0, hi0);
+        });
+        static_assert(KC % 2 == 0, "register double buffer parity");
+
+        // extras: a received parity row y adds its block to T_y; a repeated data row adds
+        // C[y][row] times its block to every syndrome row (run-time coefficients)
+        auto extra = [&](int e, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
+                         uint32_t (&nhi)[8]) __attribute__((always_inline)) {
+            WZ v;
+            advance(lo, hi, nlo, nhi, v.W8);
+            const int row = tile_cload_u8(tb + syn::kERow, e);
+            if (row >= KC) {
+                // a mask per row, not a branch: `if (y == 2t + h) acc[t] ^= ...` is folded
+                // into a computed index, which sends acc to scratch memory
+                const uint32_t ybit = 1u << (row - KC);
+                static_for<NCH>([&](auto chc) __attribute__((always_inline)) {
+                    constexpr int CH = decltype(chc)::value;
+                    if (chunk == CH) {
+                        static_for<ROWS>([&](auto tc) __attribute__((always_inline)) {
+                            constexpr int t = decltype(tc)::value, y = NCH * t + CH;
+                            if ((need >> y) & 1u) {
+                                const uint32_t mk = (ybit >> y) & 1u ? ~0u : 0u;
+#pragma unroll
+                                for (int r = 0; r < 8; ++r)
+                                    acc[t][r] ^= v.W[r] & mk;
+                            }
+                        });
+                    }
+                });
+            } else {
+                expand_wz(v);
+                static_for<NCH>([&](auto chc) __attribute__((always_inline)) {
+                    constexpr int CH = decltype(chc)::value;
+                    if (chunk == CH) {
+                        static_for<ROWS>([&](auto tc) __attribute__((always_inline)) {
+                            constexpr int t = decltype(tc)::value, y = NCH * t + CH;
+                            if ((need >> y) & 1u) {
+                                const uint32_t cf = (uint32_t)tile_cload_u8(cenc, y * KC + row);
+                                apply_nibble<0>(acc[t], cf & 15u, v);
+                                apply_nibble<4>(acc[t], cf >> 4, v);
+                            }
+                        });
+                    }
+                });
+            }
+        };
+#pragma unroll 1
+        for (int e = 0; e + 1 < ne; e += 2) {
+            extra(e, lo0, hi0, lo1, hi1);
+            extra(e + 1, lo1, hi1, lo0, hi0);
+        }
+        if (ne & 1) {
+            extra(ne - 1, lo0, hi0, lo1, hi1);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                lo0[t] = lo1[t];
+                hi0[t] = hi1[t];
+            }
+        }
+
+        // ---- E_j = sum_i Sinv[j][i] T_i.  The syndromes go through LDS, TH per round.  Up
+        // to NCH * 4 outputs (the usual case): one round, 4 outputs per wave.  More: passes of
+        // 2 outputs per wave over every round, so that only 2 x 8 output words are live next
+        // to the syndrome rows still to be exchanged (no spills at 3 waves per SIMD).  Every
+        // path issues the same store count (outputs past n with an empty range).
+        uint32_t* tlw = tl + tile * 8 * 64 + lane;   // + (i * NT * 8 + r) * 64
+        asm volatile("" ::: "memory");   // stores stay in issue order among the DMAs
+        const bool live = tile * 64 + lane < NW;
+        uint32_t vo = live && c < NWF ? 4u * (uint32_t)c : kTDrop;
+        uint32_t vt = live && c == NWF && NWF < NW ? 4u * (uint32_t)c : kTDrop;
+        asm volatile("" : "+v"(vo), "+v"(vt));
+        // this wave's syndromes i in [h0, h0 + TH) to LDS, then a workgroup barrier
+        auto exchange = [&](int h0) __attribute__((always_inline)) {
+            static_for<NCH>([&](auto chc) __attribute__((always_inline)) {
+                constexpr int CH = decltype(chc)::value;
+                if (chunk == CH) {
+                    static_for<ROWS>([&](auto tc) __attribute__((always_inline)) {
+                        constexpr int t = decltype(tc)::value, y = NCH * t + CH;
+                        if ((need >> y) & 1u) {
+                            const int ii = tile_cload_u8(tb + syn::kISlot, y) - h0;
+                            if (ii >= 0 && ii < TH) {
+#pragma unroll
+                                for (int r = 0; r < 8; ++r) tlw[(ii * NT * 8 + r) * 64] = acc[t][r];
+                            }
+                        }
+                    });
+                }
+            });
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            tile_barrier();
+        };
+        // o[q] ^= Sinv[j][i] T_i for the round's syndromes, outputs j = NCH * (q0 + q) + chunk
+        auto solve = [&](int h0, int q0, auto& o) __attribute__((always_inline)) {
+            constexpr int NQ = sizeof(o) / sizeof(o[0]);
+            static_for<TH>([&](auto ic) __attribute__((always_inline)) {
+                constexpr int ii = decltype(ic)::value;
+                __builtin_amdgcn_sched_barrier(0);   // one syndrome row live at a time
+                if (h0 + ii < n) {
+                    WZ v;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v.W[r] = tlw[(ii * NT * 8 + r) * 64];
+                    expand_wz(v);
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const int j = NCH * (q0 + q) + chunk;
+                        if (j < n) {
+                            const uint32_t cf =
+                                (uint32_t)tile_cload_u8(tb + syn::kSinv, j * 16 + h0 + ii);
+                            apply_nibble<0>(o[q], cf & 15u, v);
+                            apply_nibble<4>(o[q], cf >> 4, v);
+                        }
+                    }
+                }
+            });
+        };
+        // outputs q0 .. q0 + NQ - 1 of this wave (a fixed number of store instructions)
+        auto store = [&](int q0, const auto& o) __attribute__((always_inline)) {
+            constexpr int NQ = sizeof(o) / sizeof(o[0]);
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int j = NCH * (q0 + q) + chunk;
+                const bool on = j < n;
+                const int oslot = slots ? (on ? tile_sload_u8(slots, g * rmax + j) : 0) : j;
+                uint8_t* dst = out + g * out_gstride + (long long)oslot * BB;
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    dst, 0, on ? (unsigned)BB : 0u, 0x00020000);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const uint32_t vsum = o[q][r];
+                    __builtin_amdgcn_raw_buffer_store_b32(vsum, rs, vo, r * S, 0);
+                    if (S & 2)
+                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)vsum, rs, vt, r * S, 0);
+                    if (S & 1)
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(vsum >> (8 * (S & 2))), rs,
+                                                             vt, r * S + (S & 2), 0);
+                }
+            }
+            asm volatile("" ::: "memory");
+        };
+        static_assert(RO == 8 && TH == NCH * 4, "output passes");
+        if (n <= TH) {
+            uint32_t o[4][8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) o[q][r] = 0;
+            if (n > 0) {   // uniform: the barrier
+                exchange(0);
+                solve(0, 0, o);
+            }
+            store(0, o);
+            store(4, o);   // q >= 4: no output (j >= 8 >= n), empty range
+        } else {
+            static_for<4>([&](auto pc) __attribute__((always_inline)) {
+                constexpr int q0 = 2 * decltype(pc)::value;
+                uint32_t o[2][8];
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) o[q][r] = 0;
+#pragma unroll 1
+                for (int h0 = 0; h0 < n; h0 += TH) {
+                    exchange(h0);
+                    solve(h0, q0, o);
+                    // every wave has read this round before the next one rewrites the area
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    tile_barrier();
+                }
+                store(q0, o);
+            });
+        }
     }
     tile_wait_vmcnt<0>();
 }
@@ -344,7 +713,7 @@ bool gf_tile_supported(int k, int m, int bb, int rc, bool decode, const Tune& t)
     // encode: the compiled code only (the run-time form of this kernel spills at the
     // 10-wave occupancy it needs; other codes stay on gf_apply)
     if (!decode) return t.const_enc && k == 128 && m == 16;
-    return (std::min(k, m) + rc - 1) / rc <= 2;
+    return false;   // MEASURE: run-time decode routed to gf_apply
 }
 
 hipError_t launch_gf_tile(const uint8_t* in, uint8_t* out, const uint8_t* coef,
@@ -383,6 +752,34 @@ hipError_t launch_gf_tile(const uint8_t* in, uint8_t* out, const uint8_t* coef,
     }
 #undef QT_DEPTH
 #undef QT_GO
+    return hipGetLastError();
+}
+
+bool gf_tile_syndrome_supported(int k, int m, int bb, int rmax, const Tune& t) {
+    return t.tile && t.const_enc && k == 128 && m == 16 && bb == 8 * kTileS && rmax <= 16;
+}
+
+hipError_t launch_gf_tile_syndrome(const uint8_t* in, uint8_t* out, const uint8_t* tab,
+                                   const uint8_t* slots, const int32_t* nout,
+                                   const uint8_t* cenc, int k, int m, int bb, long long groups,
+                                   int rmax, long long tab_gstride, long long out_gstride,
+                                   hipStream_t st, const Tune& t) {
+    if (groups <= 0) return hipSuccess;
+    if (!gf_tile_syndrome_supported(k, m, bb, rmax, t) || tab_gstride < syn::kBytes)
+        return hipErrorInvalidValue;
+    if ((((uintptr_t)in) & 15) || ((((uintptr_t)tab) | (uintptr_t)tab_gstride |
+                                     (uintptr_t)cenc | (uintptr_t)slots) & 3))
+        return hipErrorInvalidValue;
+    using TS = TileShape<kTileS>;
+    constexpr int D = 6;
+    const size_t lds = (size_t)(D + 2) * TS::BBP + (size_t)8 * TS::NT * 8 * 64 * 4;
+    const unsigned threads = (unsigned)(TS::NT * 2 * 64);
+    long long cap = (long long)t.cus * std::max(1, (int)((160 * 1024) / lds));
+    if (t.tile_grid > 0) cap = t.tile_grid;
+    const unsigned grid = (unsigned)std::min<long long>(groups, cap);
+    note_kernel("gf_tile_syn_kernel<decode,k128m16>");
+    hipLaunchKernelGGL((gf_tile_syn_kernel<kTileS, D>), dim3(grid), dim3(threads), lds, st, in,
+                       out, tab, slots, nout, cenc, groups, rmax, tab_gstride, out_gstride);
     return hipGetLastError();
 }
 

@@ -440,8 +440,9 @@ def test_last_kernels_reports_launches(tuned_engine):
     engine = tuned_engine
     for (k, m, bb, enc, dec) in [
             (10, 1, 1352, "xor_dma_kernel<encode>", "xor_dma_kernel<decode,recovered>"),
-            (32, 4, 1352, "gf_stream_kernel<encode,k32m4>", "gf_stream_kernel<decode>"),
-            (32, 3, 1352, "gf_stream_kernel<encode>", "gf_stream_kernel<decode>")]:
+            (32, 4, 1352, "gf_ring_kernel<encode,k32m4>", "gf_stream_kernel<decode>"),
+            (32, 3, 1352, "gf_stream_kernel<encode>", "gf_stream_kernel<decode>"),
+            (16, 4, 1352, "gf_stream_kernel<encode>", "gf_stream_kernel<decode>")]:
         G = 8
         data = torch.from_numpy(synth.group_data(3, k, bb, G)).cuda()
         parity = torch.zeros((G, m, bb), dtype=torch.uint8, device="cuda")
@@ -588,7 +589,7 @@ def test_stream_any_small_block(engine, oracle, bb, k, m, r):
     data = synth.group_data(bb + 17 * k + m, k, bb, G)
     p_or, rc_or = oracle.encode_batch(k, m, bb, data)
     p_gpu, rc = gpu_encode(engine, k, m, bb, data)
-    assert fec.last_kernels().startswith("gf_stream_kernel<encode")
+    assert fec.last_kernels().startswith(("gf_stream_kernel<encode", "gf_ring_kernel<encode"))
     assert rc == rc_or == 0
     np.testing.assert_array_equal(p_gpu, p_or)
     rows, src = synth.loss_patterns(k, m, r, G, 3 + bb, shuffle=True)
@@ -615,10 +616,9 @@ def test_stream_any_small_block(engine, oracle, bb, k, m, r):
 @pytest.mark.parametrize("grid", [1, 3, 0])
 @pytest.mark.parametrize("k,m,r", [(128, 16, 8), (128, 16, 13), (40, 16, 16), (16, 6, 4)])
 def test_tile_many_groups_per_workgroup(tuned_engine, oracle, depth, grid, k, m, r):
-    """Config D's kernel with the grid capped so one workgroup streams several groups back
+    """Config D's kernels with the grid capped so one workgroup streams several groups back
     to back (the DMA prefetch crosses group boundaries and the previous group's stores sit
     in the vmcnt count); every third group has no loss."""
-    import torch
     engine = tuned_engine
     engine.set_option("tile_grid", grid)
     engine.set_option("tile_depth", depth)
@@ -634,10 +634,19 @@ def test_tile_many_groups_per_workgroup(tuned_engine, oracle, depth, grid, k, m,
     rows[::3] = np.arange(k, dtype=rows.dtype)
     src[::3] = np.arange(k, dtype=src.dtype)
     recv = synth.assemble_received(data, p_or, src)
+    dec_kernel = ("gf_tile_syn_kernel<decode,k128m16>" if (k, m) == (128, 16)
+                  else "gf_apply_kernel<decode")
+    check_decodes(engine, oracle, k, m, bb, recv, rows, dec_kernel)
+
+
+def check_decodes(engine, oracle, k, m, bb, recv, rows, dec_kernel):
+    """Both in-place layouts and the recovered-blocks layout against the oracle."""
+    import torch
+    G = recv.shape[0]
     b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
     for inplace in (True, False):
         b, rr, s = gpu_decode(engine, k, m, bb, recv, rows, inplace=inplace)
-        assert "gf_tile_kernel<decode>" in fec.last_kernels()
+        assert dec_kernel in fec.last_kernels()
         np.testing.assert_array_equal(s, s_or)
         np.testing.assert_array_equal(rr, r_or)
         np.testing.assert_array_equal(b, b_or)
@@ -645,8 +654,68 @@ def test_tile_many_groups_per_workgroup(tuned_engine, oracle, depth, grid, k, m,
     rmax = min(k, m)
     rec = torch.zeros((G, rmax, bb), dtype=torch.uint8, device="cuda")
     rec_rows = torch.zeros((G, rmax), dtype=torch.uint8, device="cuda")
-    engine.decode_recovered(k, m, bb, dev(recv), dev(rows), rec, rec_rows)
-    assert "gf_tile_kernel<decode>" in fec.last_kernels()
+    st = torch.full((G,), 7, dtype=torch.int32, device="cuda")
+    engine.decode_recovered(k, m, bb, dev(recv), dev(rows), rec, rec_rows, status=st)
+    assert dec_kernel in fec.last_kernels()
+    np.testing.assert_array_equal(host(st), s_or)
     np.testing.assert_array_equal(host(rec_rows), exp_rows)
     mask = exp_rows != 255
     np.testing.assert_array_equal(host(rec)[mask], exp[mask])
+    return s_or
+
+
+@pytest.mark.parametrize("grid", [1, 3, 0])
+def test_syndrome_decode_patterns(tuned_engine, oracle, grid):
+    """Config D's decode (syndromes of the compiled (128, 16) code, then the r x r solve,
+    gf_tile_syn_kernel) on hand-built receive sets: no loss, 16 losses, single and scattered
+    parity rows, more than 8 losses (two syndrome exchange rounds), a repeated data row (an
+    extra block with run-time coefficients); shuffled arrival; the grid capped so groups
+    share workgroups.  Malformed sets (a repeated parity row: singular; a row tag past
+    k + m) are where the reference's result is not defined (its elimination runs on a
+    singular bit matrix / reads past its Cauchy matrix): status -3, group left unchanged."""
+    engine = tuned_engine
+    engine.set_option("tile_grid", grid)
+    k, m, bb = 128, 16, 9008
+    rng = np.random.default_rng(90 + grid)
+    data = synth.group_data(777 + grid, k, bb, 10)
+    p_or, _ = oracle.encode_batch(k, m, bb, data)
+
+    def lose(lost, par):
+        keep = [x for x in range(k) if x not in set(lost)]
+        return keep + [k + y for y in par]
+    sets = [
+        list(range(k)),                                                  # no loss
+        lose(sorted(rng.choice(k, 16, replace=False)), list(range(16))),  # 16 losses
+        lose([77], [15]),                                                # one, last parity row
+        lose([0, 9, 64, 100, 127], [1, 3, 9, 12, 14]),                   # scattered rows
+        lose(list(range(8)), list(range(8))),                            # the bench's pattern
+        lose(sorted(rng.choice(k, 9, replace=False)), [0, 2, 4, 5, 6, 8, 10, 13, 15]),
+    ]
+    dup_data = list(range(k))                 # row 6 twice, row 5 missing, parity row 2
+    dup_data[5] = 6
+    dup_data[40] = k + 2
+    sets.append(dup_data)
+    dup_par = lose([3, 4], [3, 3])            # the same parity row twice: singular
+    sets.append(dup_par)
+    bad = lose([10], [1])
+    bad[-1] = 200                             # row tag past k + m
+    sets.append(bad)
+    sets.append(lose(sorted(rng.choice(k, 12, replace=False)), sorted(rng.choice(m, 12, replace=False))))
+    rows = np.zeros((10, k), np.uint8)
+    src = np.zeros((10, k), np.int16)
+    for g, s in enumerate(sets):
+        s = np.array(s)
+        if g % 2:
+            s = s[rng.permutation(k)]
+        rows[g] = s
+        src[g] = np.where(s < k + m, s, 0)
+    recv = synth.assemble_received(data, p_or, src)
+    ok = np.array([g not in (7, 8) for g in range(10)])
+    s_or = check_decodes(engine, oracle, k, m, bb, recv[ok], rows[ok],
+                         "gf_tile_syn_kernel<decode,k128m16>")
+    assert (s_or == 0).all()
+    bad = ~ok
+    b, rr, st = gpu_decode(engine, k, m, bb, recv[bad], rows[bad], inplace=True)
+    assert st.tolist() == [-3, -3]
+    np.testing.assert_array_equal(rr, rows[bad])
+    np.testing.assert_array_equal(b, recv[bad])

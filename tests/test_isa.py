@@ -1,6 +1,7 @@
 """ISA guard for the counted-vmcnt kernels (CPU only: hipcc cross-compiles gfx950).
 
-gf_stream_kernel (quic_amd/csrc/gf_stream.hip) and gf_tile_kernel (gf_tile.hip) keep their
+gf_stream_kernel / gf_ring_kernel (quic_amd/csrc/gf_stream.hip) and gf_tile_kernel /
+gf_tile_syn_kernel (gf_tile.hip) keep their
 own count of the VMEM instructions they issued and wait with `s_waitcnt vmcnt(N)` for
 exactly the pieces a block needs.  That is only sound if the compiler emits no VMEM
 instruction outside the count (a global_load of a uniform byte, a register spill, say) and
@@ -35,7 +36,7 @@ def stream_isa(tmp_path_factory, request):
                    check=True, capture_output=True)
     text = out.read_text()
     bodies = {}
-    for m in re.finditer(r"^(_ZN4qfec\d+" + name + r"_kernel\w+):", text, re.M):
+    for m in re.finditer(r"^(_ZN4qfec\d+gf_\w+?_kernel\w+):", text, re.M):   # every kernel
         end = text.index(".Lfunc_end", m.end())
         bodies[m.group(1)] = text[m.end():end]
     assert len(bodies) >= 3, "expected the encode and decode instantiations"
