@@ -266,9 +266,9 @@ int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
                                       (long long)m * bb, false, st, c->tune));
         return 0;
     }
-    if (qfec::gf_tile_supported(k, m, bb, rc, false, c->tune) && ((uintptr_t)d_data & 15) == 0) {
-        QF_HIP(qfec::launch_gf_tile(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc, 0, 0,
-                                    (long long)m * bb, false, st, c->tune));
+    if (qfec::gf_tile_supported(k, m, bb, c->tune) && ((uintptr_t)d_data & 15) == 0) {
+        QF_HIP(qfec::launch_gf_tile_encode(d_data, d_par, k, m, bb, G, (long long)m * bb, st,
+                                           c->tune));
         return 0;
     }
     QF_HIP(qfec::launch_gf_encode(d_data, d_par, tab, k, m, bb, G, rc, st, c->tune));
@@ -318,14 +318,6 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
         QF_HIP(qfec::launch_gf_stream(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
                                       rmax, (long long)nchunk * k * rcp, (long long)k * bb, true,
                                       st, c->tune));
-        return 0;
-    }
-    if (qfec::gf_tile_supported(k, m, bb, rc, true, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
-        // a group's stores follow all of its reads: in place needs no scratch
-        const int rcp = std::max(rc, 4);
-        QF_HIP(qfec::launch_gf_tile(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
-                                    rmax, (long long)nchunk * k * rcp, (long long)k * bb, true,
-                                    st, c->tune));
         return 0;
     }
     if (nchunk > 1 && d_out == d_blocks) {
@@ -400,14 +392,6 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
                                       c->tune));
         return 0;
     }
-    if (qfec::gf_tile_supported(k, m, bb, rc, true, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
-        const int rcp = std::max(rc, 4);
-        const int nchunk = (rmax + rc - 1) / rc;
-        QF_HIP(qfec::launch_gf_tile(d_blocks, d_rec, w.coef, nullptr, w.nout, k, m, bb, G, rc,
-                                    rmax, (long long)nchunk * k * rcp, (long long)rmax * bb,
-                                    true, st, c->tune));
-        return 0;
-    }
     QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, d_rec, w, k, m, bb, G, rc, rmax, st,
                                           c->tune));
     return 0;
@@ -429,7 +413,7 @@ int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
 // and D2H (s_out) are ordered by events, and NB staging buffers rotate, so the copy-in of
 // chunk i + 1 and the copy-out of chunk i - 1 overlap the kernels of chunk i (PCIe is
 // full duplex).  The kernels of all chunks stay on one stream, so the decode workspace is
-// never shared by two chunks in flight.  Chunk size: QFEC_HOST_CHUNK_MB (default 64).
+// never shared by two chunks in flight.  Chunk size: the host_chunk_mb option (64 MiB).
 // fn(g0, n, buf, phase): phase 0 enqueues the H2D, 1 the kernels, 2 the D2H.
 template <class F>
 int host_pipeline_body(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
@@ -535,7 +519,6 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"const_enc", &t.const_enc, 0, 1},     {"tile", &t.tile, 0, 1},
         {"stream_static", &t.stream_static, 0, 1},
         {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_depth", &t.tile_depth, 6, 12},
-        {"tile_rot", &t.tile_rot, 0, 255},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -559,7 +542,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
         {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"tile", t.tile}, {"tile_grid", t.tile_grid},
-        {"tile_depth", t.tile_depth}, {"tile_rot", t.tile_rot},
+        {"tile_depth", t.tile_depth},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb},
     };

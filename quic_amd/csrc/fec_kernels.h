@@ -25,10 +25,9 @@ struct Tune {
     int stream_grid = 0;      // gf_stream: grid cap in workgroups (0: CUs x per-CU fit)
     int stream_static = 1;    // gf_stream: compile-time ring schedule for k = 32, bb = 1352
     int const_enc = 1;        // encode kernels specialised for fixed (k, m) where compiled
-    int tile = 1;             // m > 1, 9008-byte blocks: gf_tile (0: gf_apply)
+    int tile = 1;             // (128, 16) x 9008 B: gf_tile / gf_tile_syn (0: gf_apply)
     int tile_grid = 0;        // gf_tile: grid cap in workgroups (0: CUs x per-CU fit)
     int tile_depth = 6;       // gf_tile: blocks in flight per workgroup (6 or 12)
-    int tile_rot = 37;        // gf_tile decode: per-workgroup block rotation multiplier
     int pd = 2;               // gf_apply: register pipeline depth (1..3)
     int flat = 1;             // gf_apply: lane-flat encode
     int enc_rc = 8;           // gf_apply: encode outputs per wave (2, 4, 8)
@@ -135,12 +134,12 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
                             const Tune& t);
 
 
-// Workgroup-shared LDS block stream for 9008-byte blocks, column-tile waves (gf_tile.hip).
-bool gf_tile_supported(int k, int m, int bb, int rc, bool decode, const Tune& t);
-hipError_t launch_gf_tile(const uint8_t* in, uint8_t* out, const uint8_t* coef,
-                          const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
-                          long long groups, int rc, int rmax, long long coef_gstride,
-                          long long out_gstride, bool decode, hipStream_t st, const Tune& t);
+// Workgroup-shared LDS block stream for 9008-byte blocks, column-tile waves (gf_tile.hip):
+// encode of the compiled (128, 16) code.
+bool gf_tile_supported(int k, int m, int bb, const Tune& t);
+hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, int bb,
+                                 long long groups, long long out_gstride, hipStream_t st,
+                                 const Tune& t);
 // Syndrome decode of the compiled (128, 16) code from the syn:: table (gf_tile.hip).
 bool gf_tile_syndrome_supported(int k, int m, int bb, int rmax, const Tune& t);
 hipError_t launch_gf_tile_syndrome(const uint8_t* in, uint8_t* out, const uint8_t* tab,

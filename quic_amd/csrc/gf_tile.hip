@@ -1,4 +1,4 @@
-// gf_tile.hip — m > 1 encode / decode for jumbo blocks: BASELINE config D,
+// gf_tile.hip — encode and decode of jumbo blocks: BASELINE config D,
 // (128 data + 16 parity) x 9008 B blocks (9000 B payloads, quic_fec_group.cc:344-352).
 //
 // Same bit-sliced Cauchy arithmetic as gf_stream / gf_apply (cauchy_256.cpp:90-125,
@@ -16,12 +16,12 @@
 //   (16-byte aligned pieces: bb % 16 == 0), its sub-rows are realigned in LDS (v_alignbyte),
 //   and the waves of one workgroup stay within one block of each other, which keeps the
 //   large unrolled encode program inside the instruction cache.
-// * Encode with a compiled code (KC, MC > 0: (128, 16)): the coefficients are compile-time
+// * Encode of the compiled code (KC, MC) = (128, 16): the coefficients are compile-time
 //   constants (cauchy_const.h, cauchy_256.cpp:422-480), the block loop is unrolled and every
-//   8x8 expansion folds into straight-line XORs, with no scalar nibble dispatch — about half
-//   the instructions of the run-time form, which is issue-bound on this shape.
-// * Decode: run-time coefficients (decode prep output [G][nchunk][k][RCP]) through the
-//   scalar nibble dispatch of gf_bitslice.h.
+//   8x8 expansion folds into straight-line XORs (the windowed form), with no scalar nibble
+//   dispatch — about half the instructions of the run-time form, which is issue-bound on
+//   this shape (and spills at the 10-wave occupancy; other codes stay on gf_apply).
+// * Decode: gf_tile_syn_kernel below (syndromes of the same compiled code).
 //
 // vmcnt bookkeeping: per block a wave issues exactly PPW DMA instructions; per group it
 // issues exactly RC * 8 * SPR stores (lanes of unused outputs dropped), so the count of
@@ -78,13 +78,11 @@ struct TileShape {
 };
 
 // S: sub-row bytes (compile time).  RC: outputs per chunk wave, NCH chunks.  D: blocks in
-// flight (D + 2 LDS buffers).  KC, MC > 0: encode of the compiled code (k, m) = (KC, MC).
-template <int S, int RC, int NCH, bool DECODE, int D, int KC = 0, int MC = 0>
+// flight (D + 2 LDS buffers).  Encode of the compiled code (k, m) = (KC, MC).
+template <int S, int RC, int NCH, int D, int KC, int MC>
 __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
                              (TileShape<S>::NT * NCH + 3) / 4) void gf_tile_kernel(
-    const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
-    const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
-    int k, int m, int rmax, long long coef_gstride, long long out_gstride, int rot_mul) {
+    const uint8_t* in, uint8_t* out, long long groups, long long out_gstride) {
     using T = TileShape<S>;
     constexpr int BB = T::BB, NW = T::NW, NWF = T::NWF, NT = T::NT, NPB = T::NPB;
     constexpr int BBP = T::BBP, SPR = T::SPR;
@@ -94,19 +92,14 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
     // may still have LDS reads outstanding on (a wave issues the DMA of block b + D after it
     // passed the barrier of block b, so every wave has consumed block b - 2 by then)
     constexpr int NBUF = D + 2;
-    constexpr int RCP = RC < 4 ? 4 : RC;
-    constexpr int NCW = RCP / 4;
     constexpr int NST = RC * 8 * SPR;               // stores per wave per group
-    // PIPE: block b + 1's LDS reads are issued before block b is combined (register double
-    // buffer).  The compiled encode does without it: its constant XOR program already needs
-    // ~150 VGPRs, and a 10-wave workgroup must fit 3 waves per SIMD (<= 168 VGPRs, no spills).
-    constexpr bool PIPE = true;
-    constexpr int AHEAD = PIPE ? D - 1 : D;          // blocks issued after the awaited one
+    // block b + 1's LDS reads are issued before block b is combined (register double buffer)
+    constexpr int AHEAD = D - 1;                     // blocks issued after the awaited one
     constexpr int WAITN = AHEAD * PPW;
     constexpr int WAITG = AHEAD * PPW + NST > 63 ? 63 : AHEAD * PPW + NST;
-    constexpr int SAUX = DECODE ? 0 : 2;            // encode's dense parity stream: nt stores
+    constexpr int SAUX = 2;                          // the dense parity stream: nt stores
     static_assert(S % 2 == 0 && BB % 16 == 0, "16-byte aligned blocks, 2-byte aligned sub-rows");
-    static_assert(KC == 0 || (!DECODE && MC > 0 && (MC + RC - 1) / RC == NCH), "compiled code");
+    static_assert(MC > 0 && (MC + RC - 1) / RC == NCH && KC % 2 == 0, "compiled code");
     static_assert(WAITN <= 63 && D >= 2, "pipeline depth");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
@@ -114,28 +107,20 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
     const int w = wave_id();
     const int tile = w % NT, chunk = w / NT;
     const int c = min(tile * 64 + lane, NW - 1);     // idle lanes shadow the last word
-    if constexpr (KC > 0) {
-        k = KC;
-        m = MC;
-    }
+    constexpr int k = KC;
     const long long G0 = blockIdx.x, GS = gridDim.x;
     if (G0 >= groups) return;                        // uniform over the workgroup
     const long long cnt = (groups - 1 - G0) / GS + 1;
     const long long nblocks = cnt * k;               // this workgroup's block stream
 
-    // ---- DMA side: block b of the stream = block (iss_x + rot) % k of group G0 + iss_i * GS.
-    // The run-time form may start every group at a per-workgroup block offset `rot`: the
-    // concurrently streamed groups are 1,153,024 B = 2^11 * 563 apart, so without it every
-    // workgroup reads the same offset of its group at the same time.
-    const int rot = KC > 0 ? 0 : (int)(((long long)G0 * rot_mul) % k);
+    // ---- DMA side: block b of the stream = block iss_x of group G0 + iss_i * GS
     long long iss_b = 0;
     int iss_x = 0;
     const uint8_t* iss_src = in + G0 * (long long)k * BB;
     const long long gstride = GS * (long long)k * BB;
     auto issue_next = [&]() {
         uint8_t* dst = smem + (int)(iss_b % NBUF) * BBP;
-        const int xm = iss_x + rot < k ? iss_x + rot : iss_x + rot - k;
-        const uint8_t* src = iss_src + (long long)xm * BB;
+        const uint8_t* src = iss_src + (long long)iss_x * BB;
 #pragma unroll
         for (int q = 0; q < PPW; ++q) {
             const int p = min(w + q * NWV, NPB - 1);   // surplus waves reload the last piece
@@ -154,7 +139,7 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
     // starts t * S bytes into the buffer, misaligned by (t * S) & 3, realigned at use)
     auto read_block = [&](long long b, uint32_t (&lo)[8], uint32_t (&hi)[8]) {
         uint32_t c4 = 4u * (uint32_t)c;
-        if constexpr (KC > 0) asm volatile("" : "+v"(c4));   // no hoisting across blocks
+        asm volatile("" : "+v"(c4));   // no hoisting across blocks
         const uint8_t* L = smem + (int)(b % NBUF) * BBP + c4;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -179,24 +164,14 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
     for (int u = 0; u < D; ++u)
         if (u < nblocks) issue_next();
     uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
-    if constexpr (PIPE) {
-        wait_block(0, false);
-        read_block(0, lo0, hi0);
-    }
+    wait_block(0, false);
+    read_block(0, lo0, hi0);
 
     long long b = 0;   // stream index of the current block
 #pragma unroll 1
     for (long long i = 0; i < cnt; ++i) {
         const long long g = G0 + i * GS;
-        // Encode: chunk c owns outputs c * RC + j.  Decode interleaves them, output
-        // o = NCH * j + c, so that with fewer than NCH * RC erasures every chunk's waves still
-        // share the work (8 losses of a (128, 16) group: 4 outputs each, not 8 and 0).
-        int n;
-        if (DECODE) n = min((nout[g] - chunk + NCH - 1) / NCH, RC);
-        else n = min(m - chunk * RC, RC);
-        // decode prep table [G][nchunk][k][RCP]: output o is byte o % RC of chunk o / RC
-        const uint32_t* cw = (const uint32_t*)(coef + (DECODE ? g * coef_gstride : 0)) +
-                             (DECODE ? 0 : (long long)chunk * k * NCW);
+        const int n = min(MC - chunk * RC, RC);      // chunk h owns outputs h * RC + j
         uint32_t acc[RC][8];
 #pragma unroll
         for (int j = 0; j < RC; ++j)
@@ -204,22 +179,16 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
             for (int r = 0; r < 8; ++r) acc[j][r] = 0;
 
         // one block: prefetch block b + D, pull block b + 1 into registers, combine block b
-        // xc: the block index in the group, an int or (KC > 0) an integral_constant;
-        // chc: the chunk (KC > 0: an integral_constant)
-        auto step = [&](auto xc, auto chc, uint32_t (&lo)[8], uint32_t (&hi)[8],
-                        uint32_t (&nlo)[8], uint32_t (&nhi)[8]) __attribute__((always_inline)) {
-            const int x = xc;
+        // (xc: the block index in the group, an integral_constant)
+        auto step = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
+                        uint32_t (&nhi)[8]) __attribute__((always_inline)) {
+            constexpr int x = decltype(xc)::value;
             if (b + D < nblocks) issue_next();
             // blocks 0 .. D - 1 of a group were DMA'd before the previous group's stores
             // were issued, so those stores are younger than their pieces
-            if constexpr (PIPE) {
-                if (b + 1 < nblocks) {
-                    wait_block(b + 1, i > 0 && x + 1 <= D - 1);
-                    read_block(b + 1, nlo, nhi);
-                }
-            } else {
-                wait_block(b, i > 0 && x <= D - 1);
-                read_block(b, lo, hi);
+            if (b + 1 < nblocks) {
+                wait_block(b + 1, i > 0 && x + 1 <= D - 1);
+                read_block(b + 1, nlo, nhi);
             }
             ++b;
             WZ v;
@@ -228,88 +197,39 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
                 const int o = t * S;
                 v.W[t] = (o & 3) ? __builtin_amdgcn_alignbyte(hi[t], lo[t], o & 3) : lo[t];
             }
-            if constexpr (KC > 0) {
-                // windowed form (gf_bitslice.h): one v_bitop3 per (output, sub-row); row 0 is
-                // P0, all coefficients 1 (cauchy_256.cpp:1519-1523)
-                // The blocks' common work (DMA, waits, LDS reads, the combinations) is
-                // shared; only the apply differs per chunk, behind a uniform branch.
-                Win win;
-                win_build(v.W8, win);
-                static_for<NCH>([&](auto chc2) __attribute__((always_inline)) {
-                    constexpr int CH = decltype(chc2)::value;
-                    if (chunk == CH) {
-                        static_for<RC>([&](auto jc) __attribute__((always_inline)) {
-                            constexpr int o = CH * RC + decltype(jc)::value;
-                            if constexpr (o < MC)
-                                win_apply<cauchy_coef(MC, o, decltype(xc)::value)>(
-                                    acc[decltype(jc)::value], win);
-                        });
-                    }
-                });
-                (void)chc;
-            } else {
-                if (n <= 0) return;   // no output in this chunk for this group
-                // coefficient rows of block x in every chunk: NCH x NCW dwords
-                uint32_t cwv[NCH][NCW];
-#pragma unroll
-                for (int h = 0; h < NCH; ++h)
-#pragma unroll
-                    for (int q = 0; q < NCW; ++q)
-                        cwv[h][q] = cw[((long long)h * k + (x + rot < k ? x + rot : x + rot - k)) * NCW + q];
-                expand_wz(v);
-#pragma unroll
-                for (int j = 0; j < RC; ++j) {
-                    if (j < n) {
-                        const int o = NCH * j + chunk;             // wave-uniform
-                        const int h = o / RC, pos = o % RC;
-                        uint32_t word = cwv[0][0];
-#pragma unroll
-                        for (int hh = 0; hh < NCH; ++hh)
-#pragma unroll
-                            for (int q = 0; q < NCW; ++q)
-                                if (hh == h && q == (pos >> 2)) word = cwv[hh][q];
-                        const uint32_t cf = (word >> (8 * (pos & 3))) & 0xFFu;
-                        apply_nibble<0>(acc[j], cf & 15u, v);
-                        apply_nibble<4>(acc[j], cf >> 4, v);
-                    }
+            // windowed form (gf_bitslice.h): one v_bitop3 per (output, sub-row); row 0 is P0,
+            // all coefficients 1 (cauchy_256.cpp:1519-1523).  The blocks' common work (DMA,
+            // waits, LDS reads, the combinations) is shared; only the apply differs per
+            // chunk, behind a uniform branch.
+            Win win;
+            win_build(v.W8, win);
+            static_for<NCH>([&](auto chc) __attribute__((always_inline)) {
+                constexpr int CH = decltype(chc)::value;
+                if (chunk == CH) {
+                    static_for<RC>([&](auto jc) __attribute__((always_inline)) {
+                        constexpr int o = CH * RC + decltype(jc)::value;
+                        if constexpr (o < MC)
+                            win_apply<cauchy_coef(MC, o, x)>(acc[decltype(jc)::value], win);
+                    });
                 }
-            }
-        };
-        if constexpr (KC > 0) {
-            static_for<KC>([&](auto xc) __attribute__((always_inline)) {
-                // accumulators opaque at every block boundary: with constant coefficients
-                // the XOR reassociation would otherwise merge the blocks' sums into one tree
-                // and keep every block's combinations live
-#pragma unroll
-                for (int j = 0; j < RC; ++j)
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
-                // and no instruction scheduled across blocks (register pressure)
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (decltype(xc)::value % 2 == 0)
-                    step(xc, 0, lo0, hi0, lo1, hi1);
-                else
-                    step(xc, 0, lo1, hi1, lo0, hi0);
             });
-            // KC is even: the next group's first block is in lo0/hi0 again
-            static_assert(KC % 2 == 0, "register double buffer parity");
-        } else {
-            // the run-time loop keeps the parity of the double buffer by steps of 2; an odd
-            // k leaves the next block in lo1/hi1, so it is swapped back
-#pragma unroll 1
-            for (int x = 0; x + 1 < k; x += 2) {
-                step(x, 0, lo0, hi0, lo1, hi1);
-                step(x + 1, 0, lo1, hi1, lo0, hi0);
-            }
-            if (k & 1) {
-                step(k - 1, 0, lo0, hi0, lo1, hi1);
+        };
+        static_for<KC>([&](auto xc) __attribute__((always_inline)) {
+            // accumulators opaque at every block boundary: with constant coefficients the
+            // XOR reassociation would otherwise merge the blocks' sums into one tree and keep
+            // every block's combinations live
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    lo0[t] = lo1[t];
-                    hi0[t] = hi1[t];
-                }
-            }
-        }
+            for (int j = 0; j < RC; ++j)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
+            // and no instruction scheduled across blocks (register pressure)
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (decltype(xc)::value % 2 == 0)
+                step(xc, lo0, hi0, lo1, hi1);
+            else
+                step(xc, lo1, hi1, lo0, hi0);
+        });
+        // KC is even: the next group's first block is in lo0/hi0 again
 
         // ---- outputs: a fixed number of store instructions (unused outputs, idle lanes
         // and the lanes outside a word's valid bytes are dropped)
@@ -325,10 +245,7 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
             const bool on = j < n;
-            const int o = DECODE ? NCH * j + chunk : chunk * RC + j;
-            const int oslot = (DECODE && slots) ? (on ? tile_sload_u8(slots, g * rmax + o) : 0)
-                                                : o;
-            uint8_t* dst = out + g * out_gstride + (long long)oslot * BB;
+            uint8_t* dst = out + g * out_gstride + (long long)(chunk * RC + j) * BB;
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(dst, 0, on ? (unsigned)BB : 0u, 0x00020000);
 #pragma unroll
@@ -621,26 +538,26 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
         // o[q] ^= Sinv[j][i] T_i for the round's syndromes, outputs j = NCH * (q0 + q) + chunk
         auto solve = [&](int h0, int q0, auto& o) __attribute__((always_inline)) {
             constexpr int NQ = sizeof(o) / sizeof(o[0]);
-            static_for<TH>([&](auto ic) __attribute__((always_inline)) {
-                constexpr int ii = decltype(ic)::value;
-                __builtin_amdgcn_sched_barrier(0);   // one syndrome row live at a time
-                if (h0 + ii < n) {
-                    WZ v;
+            // rolled: the branchy nibble dispatch stays a small loop body in the instruction
+            // cache (the unrolled block pass before it has evicted everything else)
+            const int iend = min(TH, n - h0);
+#pragma unroll 1
+            for (int ii = 0; ii < iend; ++ii) {
+                WZ v;
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) v.W[r] = tlw[(ii * NT * 8 + r) * 64];
-                    expand_wz(v);
+                for (int r = 0; r < 8; ++r) v.W[r] = tlw[(ii * NT * 8 + r) * 64];
+                expand_wz(v);
 #pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const int j = NCH * (q0 + q) + chunk;
-                        if (j < n) {
-                            const uint32_t cf =
-                                (uint32_t)tile_cload_u8(tb + syn::kSinv, j * 16 + h0 + ii);
-                            apply_nibble<0>(o[q], cf & 15u, v);
-                            apply_nibble<4>(o[q], cf >> 4, v);
-                        }
+                for (int q = 0; q < NQ; ++q) {
+                    const int j = NCH * (q0 + q) + chunk;
+                    if (j < n) {
+                        const uint32_t cf =
+                            (uint32_t)tile_cload_u8(tb + syn::kSinv, j * 16 + h0 + ii);
+                        apply_nibble<0>(o[q], cf & 15u, v);
+                        apply_nibble<4>(o[q], cf >> 4, v);
                     }
                 }
-            });
+            }
         };
         // outputs q0 .. q0 + NQ - 1 of this wave (a fixed number of store instructions)
         auto store = [&](int q0, const auto& o) __attribute__((always_inline)) {
@@ -707,56 +624,38 @@ namespace {
 constexpr int kTileS = 1126;   // bb = 9008: 9000-byte payloads (BASELINE config D)
 }  // namespace
 
-bool gf_tile_supported(int k, int m, int bb, int rc, bool decode, const Tune& t) {
-    if (!t.tile) return false;
-    if (bb != 8 * kTileS || rc != 8 || k < t.tile_depth + 2) return false;
-    // encode: the compiled code only (the run-time form of this kernel spills at the
-    // 10-wave occupancy it needs; other codes stay on gf_apply)
-    if (!decode) return t.const_enc && k == 128 && m == 16;
-    return false;   // MEASURE: run-time decode routed to gf_apply
+bool gf_tile_supported(int k, int m, int bb, const Tune& t) {
+    return t.tile && t.const_enc && k == 128 && m == 16 && bb == 8 * kTileS;
 }
 
-hipError_t launch_gf_tile(const uint8_t* in, uint8_t* out, const uint8_t* coef,
-                          const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
-                          long long groups, int rc, int rmax, long long coef_gstride,
-                          long long out_gstride, bool decode, hipStream_t st, const Tune& t) {
+hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, int bb,
+                                 long long groups, long long out_gstride, hipStream_t st,
+                                 const Tune& t) {
     if (groups <= 0) return hipSuccess;
-    if (!gf_tile_supported(k, m, bb, rc, decode, t)) return hipErrorInvalidValue;
-    if (((uintptr_t)in & 15) != 0 || ((uintptr_t)slots & 3) != 0) return hipErrorInvalidValue;
+    if (!gf_tile_supported(k, m, bb, t)) return hipErrorInvalidValue;
+    if (((uintptr_t)in & 15) != 0) return hipErrorInvalidValue;
     if (t.tile_depth != 6 && t.tile_depth != 12) return hipErrorInvalidValue;
     using TS = TileShape<kTileS>;
-    const int nch = decode ? (rmax + rc - 1) / rc : 2;
+    constexpr int nch = 2;
     const size_t lds = (size_t)(t.tile_depth + 2) * TS::BBP;
     const unsigned threads = (unsigned)(TS::NT * nch * 64);
-    // workgroups per CU: LDS and 16 waves (the kernels use <= 128 VGPRs)
+    // workgroups per CU: LDS and 16 waves (<= 128 VGPRs: 4 waves per SIMD)
     const int per_cu = std::max(1, std::min((int)((160 * 1024) / lds), 16 / (TS::NT * nch)));
     long long cap = (long long)t.cus * per_cu;
     if (t.tile_grid > 0) cap = t.tile_grid;              // tests: many groups per workgroup
     const unsigned grid = (unsigned)std::min<long long>(groups, cap);
-#define QT_GO(NCHV, DEC, DV, KCV, MCV)                                                          \
-    hipLaunchKernelGGL((gf_tile_kernel<kTileS, 8, NCHV, DEC, DV, KCV, MCV>), dim3(grid),         \
-                       dim3(threads), lds, st, in, out, coef, slots, nout, groups, k, m, rmax,  \
-                       coef_gstride, out_gstride, t.tile_rot)
-#define QT_DEPTH(NCHV, DEC, KCV, MCV)                                                           \
-    do {                                                                                        \
-        if (t.tile_depth == 12) QT_GO(NCHV, DEC, 12, KCV, MCV);                                 \
-        else QT_GO(NCHV, DEC, 6, KCV, MCV);                                                     \
-    } while (0)
-    if (decode) {
-        note_kernel("gf_tile_kernel<decode>");
-        if (nch == 1) QT_DEPTH(1, true, 0, 0);
-        else QT_DEPTH(2, true, 0, 0);
-    } else {
-        note_kernel("gf_tile_kernel<encode,k128m16>");
-        QT_DEPTH(2, false, 128, 16);
-    }
-#undef QT_DEPTH
-#undef QT_GO
+    note_kernel("gf_tile_kernel<encode,k128m16>");
+    if (t.tile_depth == 12)
+        hipLaunchKernelGGL((gf_tile_kernel<kTileS, 8, nch, 12, 128, 16>), dim3(grid), dim3(threads),
+                           lds, st, in, out, groups, out_gstride);
+    else
+        hipLaunchKernelGGL((gf_tile_kernel<kTileS, 8, nch, 6, 128, 16>), dim3(grid), dim3(threads),
+                           lds, st, in, out, groups, out_gstride);
     return hipGetLastError();
 }
 
 bool gf_tile_syndrome_supported(int k, int m, int bb, int rmax, const Tune& t) {
-    return t.tile && t.const_enc && k == 128 && m == 16 && bb == 8 * kTileS && rmax <= 16;
+    return gf_tile_supported(k, m, bb, t) && rmax <= 16;
 }
 
 hipError_t launch_gf_tile_syndrome(const uint8_t* in, uint8_t* out, const uint8_t* tab,

@@ -394,7 +394,7 @@ OPTION_SETS = [
     {"dma": 0}, {"stream": 0}, {"stream": 0, "pd": 1}, {"stream": 0, "pd": 3},
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
     {"stream_ring": 36}, {"host_chunk_mb": 1}, {"const_enc": 0}, {"tile": 0},
-    {"tile_depth": 12}, {"tile_rot": 0}, {"stream_static": 0},
+    {"tile_depth": 12}, {"stream_static": 0},
 ]
 
 
