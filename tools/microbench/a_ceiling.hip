@@ -45,7 +45,11 @@ constexpr int NP = (GB + 1023) / 1024;          // 14 pieces
 // whole groups into NSLOT slots per wave; STORE: write a 1352-B block per group (nt)
 // SPOL: store policy 0 = nt, 1 = plain write-back; BLOCKED: wave w takes a contiguous
 // run of groups instead of g0, g0 + W, ...
-template <int NSLOT, bool STORE, int AUX, int SPOL = 0, bool BLOCKED = false>
+// XMAP: 1 = logical wave ids XCD-major (hardware deals workgroups round-robin over the 8
+// XCDs), so groups g and g + 1 run on the same XCD and a 128-B output line shared by two
+// groups is written through ONE L2; 2 = the same plus a line-padded output stride (1408 B,
+// every group's output whole lines: the upper bound of removing shared lines)
+template <int NSLOT, bool STORE, int AUX, int SPOL = 0, bool BLOCKED = false, int XMAP = 0>
 __global__ __launch_bounds__(256) void grp_kernel(const uint8_t* in, uint8_t* out, long long groups,
                                                   uint32_t* sink) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -54,7 +58,12 @@ __global__ __launch_bounds__(256) void grp_kernel(const uint8_t* in, uint8_t* ou
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     uint8_t* myl = smem + (size_t)w * NSLOT * SLOT;
     const long long nw = (long long)gridDim.x * nwv;
-    const long long wid = (long long)blockIdx.x * nwv + w;
+    long long wid = (long long)blockIdx.x * nwv + w;
+    if (XMAP) {   // requires gridDim.x % 8 == 0
+        const int nbx = gridDim.x >> 3, x = blockIdx.x & 7, j = blockIdx.x >> 3;
+        wid = ((long long)x * nbx + j) * nwv + w;
+    }
+    constexpr int OST = XMAP == 2 ? 1408 : BB;
     long long W = nw, g0 = wid, cnt;
     if (BLOCKED) {
         const long long per = (groups + nw - 1) / nw;
@@ -91,7 +100,7 @@ __global__ __launch_bounds__(256) void grp_kernel(const uint8_t* in, uint8_t* ou
         }
         const uint8_t* L = myl + u * SLOT;
         if (STORE) {
-            uint8_t* o = out + (g0 + i * W) * BB;
+            uint8_t* o = out + (g0 + i * W) * OST;
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 const int q = min(lane + 64 * j, BB / 8 - 1);
@@ -186,7 +195,7 @@ int main() {
     uint8_t *in, *out;
     uint32_t* sink;
     CK(hipMalloc(&in, in_bytes + 4096));
-    CK(hipMalloc(&out, out_bytes + 4096));
+    CK(hipMalloc(&out, (size_t)G * 1408 + 4096));
     CK(hipMalloc(&sink, 64));
     CK(hipMemset(in, 0x5a, in_bytes));
     int cus = 0;
@@ -198,18 +207,20 @@ int main() {
     };
     char nm[128];
     // grp: slots x waves (one workgroup per CU), read only and with the A stores
-#define GRPX(NSLOT, WV, ST, AUX, SP, BL, WPC)                                               \
+#define GRPX(NSLOT, WV, ST, AUX, SP, BL, WPC) GRPM(NSLOT, WV, ST, AUX, SP, BL, WPC, 0)
+#define GRPM(NSLOT, WV, ST, AUX, SP, BL, WPC, XM)                                           \
     {                                                                                       \
         const size_t lds = (size_t)WV * NSLOT * NP * 1024;                                  \
         if (lds * WPC <= 160 * 1024) {                                                      \
-            auto kern = grp_kernel<NSLOT, ST, AUX, SP, BL>;                                 \
+            auto kern = grp_kernel<NSLOT, ST, AUX, SP, BL, XM>;                                 \
             if (lds > 64 * 1024)                                                            \
                 CK(hipFuncSetAttribute((const void*)kern,                                   \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
             const unsigned nb = (unsigned)std::min<long long>((G + WV - 1) / WV, cus * WPC); \
             double ms = time_ms([&] { kern<<<nb, WV * 64, lds>>>(in, out, G, sink); }, reps); \
-            snprintf(nm, sizeof nm, "grp s=%d w=%d x%d %s aux=%d st=%s%s", NSLOT, WV, WPC,  \
-                     ST ? "rd+wr" : "rd", AUX, SP ? "wb" : "nt", BL ? " blocked" : "");    \
+            snprintf(nm, sizeof nm, "grp s=%d w=%d x%d %s aux=%d st=%s%s%s", NSLOT, WV, WPC,\
+                     ST ? "rd+wr" : "rd", AUX, SP ? "wb" : "nt", BL ? " blocked" : "",     \
+                     XM == 1 ? " xcd" : XM == 2 ? " xcd+pad" : "");                       \
             report(nm, ms, in_bytes + (ST ? out_bytes : 0));                                \
         }                                                                                   \
     }
@@ -221,6 +232,11 @@ int main() {
     GRPX(2, 1, true, 2, 0, true, 1) GRPX(2, 3, true, 2, 0, true, 1)
     GRPX(3, 1, true, 2, 0, true, 1)
     GRP(2, 1, false, 2) GRP(2, 3, false, 2)
+    GRPM(2, 1, true, 2, 0, false, 1, 1) GRPM(2, 3, true, 2, 0, false, 1, 1)
+    GRPM(2, 1, true, 2, 1, false, 1, 1) GRPM(2, 3, true, 2, 1, false, 1, 1)
+    GRPM(2, 1, true, 2, 0, false, 1, 2) GRPM(2, 3, true, 2, 0, false, 1, 2)
+    GRPM(2, 1, true, 2, 0, false, 2, 1) GRPM(3, 1, true, 2, 0, false, 1, 1)
+    GRP(2, 1, true, 2) GRP(2, 3, true, 2)
     // ring: read only, NS slots x waves per workgroup (workgroups fill the CU by LDS)
 #define RING(NS, WV, AUX)                                                                   \
     {                                                                                       \
