@@ -167,10 +167,11 @@ def loopback_config0():
 
 # Which template argument of each kernel says "decode" (bool): the PMC summaries are split
 # into the encode and the decode phase by it.
-_DECODE_ARG = {"xor_dma_kernel": 2, "gf_apply_kernel": 1, "gf_ring_kernel": 5,
-               "gf_stage_kernel": 1, "gf_stream_kernel": 2}
+_DECODE_ARG = {"xor_dma_kernel": 2, "gf_apply_kernel": 1, "gf_ring_kernel": 3,
+               "gf_stream_kernel": 2}
 _DECODE_ONLY = ("decode_prep_kernel", "decode_prep_lane_kernel", "m1_prep_kernel",
-                "scatter_recovered_kernel", "rows_k1_kernel")
+                "scatter_recovered_kernel", "rows_k1_kernel", "gf_tile_syn_kernel")
+_ENCODE_ONLY = ("replicate_kernel", "gf_tile_kernel")
 
 
 class DeviceEvents:
@@ -231,8 +232,11 @@ def _phase(name):
         return "decode"
     if kern in _DECODE_ARG and "<" in base:
         args = [a.strip() for a in base[base.index("<") + 1:base.rindex(">")].split(",")]
-        return "decode" if args[_DECODE_ARG[kern]] == "true" else "encode"
-    return "encode" if kern == "replicate_kernel" else None
+        i = _DECODE_ARG[kern]
+        if i >= len(args) or args[i] not in ("true", "false"):
+            raise ValueError(f"bench._phase: no decode flag at template argument {i} of {base}")
+        return "decode" if args[i] == "true" else "encode"
+    return "encode" if kern in _ENCODE_ONLY else None
 
 
 def pmc_traffic(workload, phase, groups):

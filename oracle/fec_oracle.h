@@ -65,6 +65,22 @@ void oracle_fill_stream(uint64_t seed, uint64_t byte_offset, uint8_t *out, uint6
 /* Monotonic wall clock in seconds (for the CPU baseline). */
 double oracle_now(void);
 
+/* Packet protection next to the FEC path (pp_oracle.c; null_encrypter.cc:23-43,
+ * null_decrypter.cc, quic_utils.cc:38-56,110-125,175-181).  out[0] = low, out[1] = high. */
+void oracle_fnv1a_128_two(const uint8_t *d1, long long l1, const uint8_t *d2, long long l2,
+                          uint64_t out[2]);
+long long oracle_null_seal(const uint8_t *ad, long long ad_len, const uint8_t *pt,
+                           long long pt_len, uint8_t *out, long long max_out);
+long long oracle_null_open(const uint8_t *ad, long long ad_len, const uint8_t *ct,
+                           long long ct_len, uint8_t *out, long long max_out);
+void oracle_null_seal_batch(long long n, const uint8_t *ad, long long ad_stride,
+                            const int32_t *ad_len, const uint8_t *in, long long in_stride,
+                            const int32_t *in_len, uint8_t *out, long long out_stride,
+                            int32_t *res);
+void oracle_null_open_batch(long long n, const uint8_t *in, long long in_stride,
+                            const int32_t *in_len, const int32_t *ad_len, uint8_t *out,
+                            long long out_stride, int32_t *res);
+
 #ifdef __cplusplus
 }
 #endif
