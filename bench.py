@@ -258,6 +258,52 @@ def pmc_traffic(workload, phase, groups):
     return round(tot * groups / d["groups"]), os.path.relpath(files[-1], ROOT)
 
 
+def packet_protection(eng, k, m, bb, data, parity, steps, stream):
+    """The step next to the codec: SerializeFec's encode + seal of the
+    G*m FEC packets (qfec_encode_seal_batch: header || NullEncrypter tag || parity), and the
+    receiver's NullDecrypter open of those packets.  Timed with events on the launch stream;
+    reported beside the bench line, never `value`."""
+    import torch
+    G = data.shape[0]
+    n, hl = G * m, 16
+    stride = (hl + 12 + bb + 3) // 4 * 4
+    dev = data.device
+    hdr = torch.arange(n * hl, dtype=torch.int32, device=dev).to(torch.uint8).view(n, hl)
+    pkt = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    pkt_len = torch.empty(n, dtype=torch.int32, device=dev)
+    # the reference's decrypter copies the whole ciphertext to its output first
+    plain = torch.empty((n, (bb + 12 + 3) // 4 * 4), dtype=torch.uint8, device=dev)
+    plen = torch.empty(n, dtype=torch.int32, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    t = {"encode": 0.0, "encode_seal": 0.0, "open": 0.0}
+    for i in range(steps + 1):
+        ev[0].record(stream)
+        eng.encode(k, m, bb, data, parity)
+        ev[1].record(stream)
+        eng.encode_seal(k, m, bb, data, parity, hdr, hl, pkt, pkt_len)
+        ev[2].record(stream)
+        eng.null_open(pkt, pkt_len, hl, plain, plen)
+        ev[3].record(stream)
+        torch.cuda.synchronize(dev)
+        if i:   # the first pass is warmup
+            t["encode"] += ev[0].elapsed_time(ev[1]) / steps
+            t["encode_seal"] += ev[1].elapsed_time(ev[2]) / steps
+            t["open"] += ev[2].elapsed_time(ev[3]) / steps
+    ok = bool((plen == bb).all()) and torch.equal(plain[:, :bb], parity.view(n, bb))
+    seal_ms = max(t["encode_seal"] - t["encode"], 1e-9)
+    pkt_bytes = n * (hl + 12 + bb)
+    return {"packets": n, "header_bytes": hl, "encrypter": "NullEncrypter (FNV-1a-128 tag)",
+            "encode_ms": round(t["encode"], 5), "encode_seal_ms": round(t["encode_seal"], 5),
+            "seal_ms": round(seal_ms, 5), "open_ms": round(t["open"], 5),
+            "seal_Mpkt_s": round(n / seal_ms / 1e3, 2),
+            "open_Mpkt_s": round(n / t["open"] / 1e3, 2),
+            "seal_GBps": round(pkt_bytes / seal_ms / 1e6, 1),
+            "open_GBps": round(pkt_bytes / t["open"] / 1e6, 1),
+            "round_trip_ok": ok,
+            "note": "seal_ms = encode_seal - encode (same stream, events); one lane per packet "
+                    "(serial FNV chain), DESIGN.md 6.2"}
+
+
 def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps, recovered):
     """Host-resident rate: pinned host buffers in and out, H2D + kernels + D2H through the
     library's pipelined host-pointer entry points (qfec_*_batch_host).  Never `value`."""
@@ -334,6 +380,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check recovered data after timing")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) leg")
+    ap.add_argument("--pp", action="store_true",
+                    help="also time the packet-protection step (encode + NullEncrypter seal of "
+                         "the FEC packets, open)")
     ap.add_argument("--host-groups", type=int, default=None,
                     help="groups in the host-inclusive leg (default: all, at most 4 GB)")
     ap.add_argument("--decode-layout", default="recovered", choices=["recovered", "slots"],
@@ -530,6 +579,10 @@ def main():
         host = host_inclusive(eng, k, m, bb, payload, data[:hg], blocks[:hg], rows[:hg],
                               args.host_steps, recovered)
 
+    pp = None
+    if rank == 0 and world == 1 and args.pp:
+        pp = packet_protection(eng, k, m, bb, data, parity, args.steps, stream)
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -581,6 +634,8 @@ def main():
             "cpu_reference_config0": cfg0,
             "host_inclusive": host,
         }
+        if pp is not None:
+            line["packet_protection"] = pp
         if verified is not None:
             line["verified"] = verified
         print(json.dumps(line), flush=True)

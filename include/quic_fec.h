@@ -134,6 +134,53 @@ QFEC_API int qfec_decode_batch_recovered_host(qfec_ctx *ctx, int k, int m, int b
                                      unsigned char *h_rec_rows, int *h_status);
 
 /* ---------------------------------------------------------------------------------
+ * Packet protection next to the FEC path (SURVEY.md §8 f, rank 4).
+ *
+ * The reference encrypts every packet after serialisation -- the FEC packets right after
+ * the encode (QuicPacketCreator::SerializeFec -> QuicFramer::EncryptInPlace,
+ * quic_packet_creator.cc:948-953, quic_framer.cc:1921-1939) -- and decrypts before the
+ * group sees a packet (quic_framer.cc:657).  In this fork QuicEncrypter::Create yields
+ * NullEncrypter for kNULL and an identity copy for every negotiated AEAD
+ * (crypto/quic_encrypter.cc:18-29), so NullEncrypter is the packet protection with
+ * arithmetic: tag12 = low 12 bytes of FNV-1a-128(AD || PT) (null_encrypter.cc:23-43,
+ * quic_utils.cc:38-56,110-125,175-181).
+ *
+ * Batches of n packets, all device pointers.  Per-packet lengths come from the int32 arrays,
+ * or, where an array is NULL, from the `_all` scalar.  d_out and out_stride must be 4-byte
+ * aligned.  d_out_len[i] = bytes written for packet i, or -1 where the reference returns
+ * false.
+ * ------------------------------------------------------------------------------- */
+/* NullEncrypter::EncryptPacket in the EncryptInPlace layout: packet i is
+ * AD_i || tag12 || PT_i at d_out + i*out_stride (AD_i at d_ad + i*ad_stride, PT_i at
+ * d_pt + i*pt_stride).  -1 (nothing written) when it does not fit in out_stride. */
+QFEC_API int qfec_null_seal_batch(qfec_ctx *ctx, long long n, const unsigned char *d_ad,
+                                  long long ad_stride, const int *d_ad_len, int ad_len_all,
+                                  const unsigned char *d_pt, long long pt_stride,
+                                  const int *d_pt_len, int pt_len_all, unsigned char *d_out,
+                                  long long out_stride, int *d_out_len, void *stream);
+/* NullDecrypter::DecryptPacket: wire packet i at d_pkt + i*pkt_stride (pkt_len bytes, the
+ * first ad_len of them the associated data).  The output first receives the ciphertext, as
+ * in the reference.  Accepted: the plaintext overwrites its start (the last 12 ciphertext
+ * bytes stay behind it) and d_out_len[i] is the plaintext length.  Rejected (ciphertext
+ * shorter than 12 bytes or tag mismatch): -1, the output holds the ciphertext copy; -1 with
+ * nothing written when the ciphertext exceeds out_stride. */
+QFEC_API int qfec_null_open_batch(qfec_ctx *ctx, long long n, const unsigned char *d_pkt,
+                                  long long pkt_stride, const int *d_pkt_len, int pkt_len_all,
+                                  const int *d_ad_len, int ad_len_all, unsigned char *d_out,
+                                  long long out_stride, int *d_out_len, void *stream);
+/* Sender side of SerializeFec (quic_packet_creator.cc:935-957): encode the groups into
+ * d_parity [G][m][bb] (qfec_encode_batch), then seal parity block (g, i) as FEC packet
+ * g*m + i with header g*m + i (d_hdr + (g*m+i)*hdr_stride) as the associated data:
+ * d_pkt + (g*m+i)*pkt_stride = header || tag12 || parity.  One call, two launches on one
+ * stream; the parity does not leave the device. */
+QFEC_API int qfec_encode_seal_batch(qfec_ctx *ctx, int k, int m, int block_bytes,
+                                    long long groups, const unsigned char *d_data,
+                                    unsigned char *d_parity, const unsigned char *d_hdr,
+                                    long long hdr_stride, const int *d_hdr_len, int hdr_len_all,
+                                    unsigned char *d_pkt, long long pkt_stride, int *d_pkt_len,
+                                    void *stream);
+
+/* ---------------------------------------------------------------------------------
  * Support: the coefficient tables, a seeded synthetic workload, diagnostics.
  * ------------------------------------------------------------------------------- */
 /* Rows 1..m-1 of the Cauchy matrix the reference selects (cauchy_256.cpp:422-480),

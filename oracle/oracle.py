@@ -184,3 +184,80 @@ def decode_blocks(k, m, bb, blocks, rows, use_ref=False):
 
 def now():
     return lib().oracle_now()
+
+
+# ---- packet protection (pp_oracle.c: NullEncrypter / NullDecrypter, FNV-1a-128)
+def _pp_lib():
+    L = lib()
+    if not getattr(L, "_pp_ready", False):
+        vp, ll = ctypes.c_void_p, ctypes.c_longlong
+        L.oracle_fnv1a_128_two.argtypes = [vp, ll, vp, ll, vp]
+        L.oracle_null_seal.restype = ll
+        L.oracle_null_seal.argtypes = [vp, ll, vp, ll, vp, ll]
+        L.oracle_null_open.restype = ll
+        L.oracle_null_open.argtypes = [vp, ll, vp, ll, vp, ll]
+        L.oracle_null_seal_batch.argtypes = [ll, vp, ll, vp, vp, ll, vp, vp, ll, vp]
+        L.oracle_null_open_batch.argtypes = [ll, vp, ll, vp, vp, vp, ll, vp]
+        L._pp_ready = True
+    return L
+
+
+def _buf(b):
+    a = np.frombuffer(bytes(b), np.uint8).copy() if not isinstance(b, np.ndarray) else b
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def fnv1a_128(d1, d2=None):
+    """QuicUtils::FNV1a_128_Hash_Two as a Python int (quic_utils.cc:110-125)."""
+    a = _buf(d1)
+    out = np.zeros(2, np.uint64)
+    if d2 is None:
+        _pp_lib().oracle_fnv1a_128_two(_ptr(a), a.size, None, 0, _ptr(out))
+    else:
+        b = _buf(d2)
+        _pp_lib().oracle_fnv1a_128_two(_ptr(a), a.size, _ptr(b), b.size, _ptr(out))
+    return int(out[0]) | (int(out[1]) << 64)
+
+
+def null_seal(ad, pt, max_out=1 << 16):
+    """NullEncrypter::EncryptPacket: bytes tag12 || PT, or None (null_encrypter.cc:23-43)."""
+    a, p = _buf(ad), _buf(pt)
+    out = np.zeros(max(max_out, 1), np.uint8)
+    n = _pp_lib().oracle_null_seal(_ptr(a), a.size, _ptr(p), p.size, _ptr(out), max_out)
+    return None if n < 0 else out[:n].tobytes()
+
+
+def null_open(ad, ct, max_out=1 << 16):
+    """NullDecrypter::DecryptPacket: (plaintext or None, output buffer bytes)."""
+    a, c = _buf(ad), _buf(ct)
+    out = np.zeros(max(max_out, c.size, 1), np.uint8)
+    n = _pp_lib().oracle_null_open(_ptr(a), a.size, _ptr(c), c.size, _ptr(out), max_out)
+    return (None if n < 0 else out[:n].tobytes()), out
+
+
+def null_seal_batch(ad, ad_len, pt, pt_len, out_stride):
+    """Batch seal in the GPU ABI layout: ad [n][*], pt [n][*] uint8, lengths int32 [n].
+    Returns (out [n][out_stride] (zeros where nothing was written), res int32 [n])."""
+    ad, pt = np.ascontiguousarray(ad, np.uint8), np.ascontiguousarray(pt, np.uint8)
+    ad_len = np.ascontiguousarray(ad_len, np.int32)
+    pt_len = np.ascontiguousarray(pt_len, np.int32)
+    n = ad.shape[0]
+    out = np.zeros((n, out_stride), np.uint8)
+    res = np.zeros(n, np.int32)
+    _pp_lib().oracle_null_seal_batch(n, _ptr(ad), ad.strides[0] if n else 0, _ptr(ad_len),
+                                     _ptr(pt), pt.strides[0] if n else 0, _ptr(pt_len),
+                                     _ptr(out), out_stride, _ptr(res))
+    return out, res
+
+
+def null_open_batch(pkt, pkt_len, ad_len, out_stride):
+    """Batch open: wire packets pkt [n][*], lengths int32 [n].  Returns (out, res)."""
+    pkt = np.ascontiguousarray(pkt, np.uint8)
+    pkt_len = np.ascontiguousarray(pkt_len, np.int32)
+    ad_len = np.ascontiguousarray(ad_len, np.int32)
+    n = pkt.shape[0]
+    out = np.zeros((n, out_stride), np.uint8)
+    res = np.zeros(n, np.int32)
+    _pp_lib().oracle_null_open_batch(n, _ptr(pkt), pkt.strides[0] if n else 0, _ptr(pkt_len),
+                                     _ptr(ad_len), _ptr(out), out_stride, _ptr(res))
+    return out, res

@@ -99,8 +99,8 @@ void oracle_null_seal_batch(long long n, const uint8_t *ad, long long ad_stride,
     for (long long i = 0; i < n; ++i) {
         uint8_t *o = out + i * out_stride;
         const long long al = ad_len[i];
-        if (out_stride < al) {
-            res[i] = -1;
+        if (al < 0 || in_len[i] < 0 || out_stride < al + 12 + in_len[i]) {
+            res[i] = -1; /* nothing written */
             continue;
         }
         memcpy(o, ad + i * ad_stride, (size_t)al);

@@ -54,6 +54,15 @@ SIGNATURES = {
                                                         ctypes.c_longlong, ctypes.c_void_p,
                                                         ctypes.c_void_p, ctypes.c_void_p,
                                                         ctypes.c_void_p, ctypes.c_void_p]),
+    "qfec_null_seal_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p]),
+    "qfec_null_open_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
+                                            ctypes.c_void_p]),
+    "qfec_encode_seal_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_longlong,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
+                                              ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p]),
     "qfec_cauchy_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "qfec_synth_fill": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_ulonglong, ctypes.c_ulonglong,
                                        ctypes.c_ulonglong, ctypes.c_void_p]),

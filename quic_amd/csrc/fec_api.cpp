@@ -627,6 +627,66 @@ int qfec_decode_batch_recovered(qfec_ctx* c, int k, int m, int bb, long long gro
                                  (int32_t*)d_status, pick(c, stream));
 }
 
+// ---- packet protection (pp_null.hip; null_encrypter.cc:23-43, null_decrypter.cc)
+int qfec_null_seal_batch(qfec_ctx* c, long long n, const unsigned char* d_ad, long long ad_stride,
+                         const int* d_ad_len, int ad_len_all, const unsigned char* d_pt,
+                         long long pt_stride, const int* d_pt_len, int pt_len_all,
+                         unsigned char* d_out, long long out_stride, int* d_out_len,
+                         void* stream) {
+    if (!c) return fail(-2, "null context");
+    if (n < 0 || ad_stride < 0 || pt_stride < 0 || out_stride < 0) return fail(-2, "bad n / stride");
+    if (n && (!d_out || !d_out_len || (!d_ad && (d_ad_len || ad_len_all)) || (!d_pt && (d_pt_len || pt_len_all))))
+        return fail(-2, "null buffer");
+    if ((((uintptr_t)d_out) | (uintptr_t)out_stride) & 3) return fail(-2, "out / out_stride not 4-byte aligned");
+    std::lock_guard<std::mutex> lk(c->mu);
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    QF_HIP(qfec::launch_null_seal(n, d_ad, ad_stride, (const int32_t*)d_ad_len, ad_len_all, d_pt,
+                                  pt_stride, (const int32_t*)d_pt_len, pt_len_all, d_out,
+                                  out_stride, (int32_t*)d_out_len, pick(c, stream)));
+    return 0;
+}
+
+int qfec_null_open_batch(qfec_ctx* c, long long n, const unsigned char* d_pkt, long long pkt_stride,
+                         const int* d_pkt_len, int pkt_len_all, const int* d_ad_len,
+                         int ad_len_all, unsigned char* d_out, long long out_stride,
+                         int* d_out_len, void* stream) {
+    if (!c) return fail(-2, "null context");
+    if (n < 0 || pkt_stride < 0 || out_stride < 0) return fail(-2, "bad n / stride");
+    if (n && (!d_pkt || !d_out || !d_out_len)) return fail(-2, "null buffer");
+    if ((((uintptr_t)d_out) | (uintptr_t)out_stride) & 3) return fail(-2, "out / out_stride not 4-byte aligned");
+    std::lock_guard<std::mutex> lk(c->mu);
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    QF_HIP(qfec::launch_null_open(n, d_pkt, pkt_stride, (const int32_t*)d_pkt_len, pkt_len_all,
+                                  (const int32_t*)d_ad_len, ad_len_all, d_out, out_stride,
+                                  (int32_t*)d_out_len, pick(c, stream)));
+    return 0;
+}
+
+int qfec_encode_seal_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
+                           const unsigned char* d_data, unsigned char* d_parity,
+                           const unsigned char* d_hdr, long long hdr_stride, const int* d_hdr_len,
+                           int hdr_len_all, unsigned char* d_pkt, long long pkt_stride,
+                           int* d_pkt_len, void* stream) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    if (groups && (!d_data || !d_parity || !d_pkt || !d_pkt_len || (!d_hdr && (d_hdr_len || hdr_len_all))))
+        return fail(-2, "null buffer");
+    if (hdr_stride < 0 || pkt_stride < 0) return fail(-2, "bad stride");
+    if ((((uintptr_t)d_pkt) | (uintptr_t)pkt_stride) & 3) return fail(-2, "pkt / pkt_stride not 4-byte aligned");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    const hipStream_t st = pick(c, stream);
+    // SerializeFec (quic_packet_creator.cc:935-957): parity packets from the group's encode,
+    // each sealed with its packet header as the associated data; packet (g, i) = g * m + i
+    if ((rc = encode_impl(c, k, m, bb, groups, d_data, d_parity, st))) return rc;
+    QF_HIP(qfec::launch_null_seal(groups * m, d_hdr, hdr_stride, (const int32_t*)d_hdr_len,
+                                  hdr_len_all, d_parity, bb, nullptr, bb, d_pkt, pkt_stride,
+                                  (int32_t*)d_pkt_len, st));
+    return 0;
+}
+
 int qfec_decode_batch_recovered_host(qfec_ctx* c, int k, int m, int bb, long long groups,
                                      const unsigned char* h_blocks, const unsigned char* h_rows,
                                      unsigned char* h_rec, unsigned char* h_rec_rows,

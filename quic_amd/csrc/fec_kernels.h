@@ -155,4 +155,16 @@ hipError_t launch_synth_gather(const uint8_t* data, const uint8_t* parity, const
                                uint8_t* blocks, int k, int m, int bb, long long groups,
                                hipStream_t st);
 
+// Packet protection (pp_null.hip): NullEncrypter seal / NullDecrypter open over n packets.
+// Per-packet lengths come from the arrays, or from the `_all` scalar when an array is null.
+// out and out_stride must be 4-byte aligned.
+hipError_t launch_null_seal(long long n, const uint8_t* ad, long long ad_stride,
+                            const int32_t* ad_len, int ad_all, const uint8_t* pt,
+                            long long pt_stride, const int32_t* pt_len, int pt_all, uint8_t* out,
+                            long long out_stride, int32_t* out_len, hipStream_t st);
+hipError_t launch_null_open(long long n, const uint8_t* pkt, long long pkt_stride,
+                            const int32_t* pkt_len, int pkt_all, const int32_t* ad_len,
+                            int ad_all, uint8_t* out, long long out_stride, int32_t* out_len,
+                            hipStream_t st);
+
 }  // namespace qfec

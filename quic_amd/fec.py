@@ -174,6 +174,56 @@ class FecEngine:
             raise FecError(rc, "qfec_decode_batch_recovered")
         return rc
 
+    # packet protection next to the codec (NullEncrypter / NullDecrypter, pp_null.hip)
+    @staticmethod
+    def _lens(lens):
+        """(array pointer, scalar) for a per-packet length argument: an int32 device
+        tensor, or an int meaning the same length for every packet."""
+        if isinstance(lens, int):
+            return None, lens
+        return _dptr(lens), 0
+
+    def null_seal(self, ad, ad_len, pt, pt_len, out, out_len, stream=None):
+        """NullEncrypter::EncryptPacket over n packets: ad [n][ad_stride], pt [n][pt_stride]
+        -> out [n][out_stride] = AD || tag12 || PT; out_len int32 [n] (-1: does not fit).
+        ad_len / pt_len: int32 [n] tensors or ints (null_encrypter.cc:23-43)."""
+        n = out.shape[0]
+        a, a_all = self._lens(ad_len)
+        p, p_all = self._lens(pt_len)
+        rc = self.lib.qfec_null_seal_batch(self._h, n, _dptr(ad), ad.stride(0) if n else 0, a,
+                                           a_all, _dptr(pt), pt.stride(0) if n else 0, p, p_all,
+                                           _dptr(out), out.stride(0), _dptr(out_len),
+                                           _stream(stream, out))
+        if rc:
+            raise FecError(rc, "qfec_null_seal_batch")
+
+    def null_open(self, pkt, pkt_len, ad_len, out, out_len, stream=None):
+        """NullDecrypter::DecryptPacket over n wire packets pkt [n][pkt_stride] (first ad_len
+        bytes = associated data) -> plaintext in out [n][out_stride], out_len int32 [n]
+        (-1: rejected)."""
+        n = pkt.shape[0]
+        p, p_all = self._lens(pkt_len)
+        a, a_all = self._lens(ad_len)
+        rc = self.lib.qfec_null_open_batch(self._h, n, _dptr(pkt), pkt.stride(0), p, p_all, a,
+                                           a_all, _dptr(out), out.stride(0), _dptr(out_len),
+                                           _stream(stream, pkt))
+        if rc:
+            raise FecError(rc, "qfec_null_open_batch")
+
+    def encode_seal(self, k, m, block_bytes, data, parity, hdr, hdr_len, pkt, pkt_len,
+                    stream=None):
+        """SerializeFec on the device: encode data [G][k][bb] into parity [G][m][bb], then
+        seal FEC packet g*m+i = hdr[g*m+i][:hdr_len] || tag12 || parity[g][i] into
+        pkt [G*m][pkt_stride]; pkt_len int32 [G*m]."""
+        G = data.shape[0]
+        h, h_all = self._lens(hdr_len)
+        rc = self.lib.qfec_encode_seal_batch(self._h, k, m, block_bytes, G, _dptr(data),
+                                             _dptr(parity), _dptr(hdr), hdr.stride(0), h, h_all,
+                                             _dptr(pkt), pkt.stride(0), _dptr(pkt_len),
+                                             _stream(stream, data))
+        if rc:
+            raise FecError(rc, "qfec_encode_seal_batch")
+
     # host-pointer batch calls (synchronous; include H2D/D2H)
     def encode_host(self, k, m, block_bytes, data):
         data = np.ascontiguousarray(data, dtype=np.uint8)

@@ -1,0 +1,7 @@
+B="python bench.py --no-cpu-baseline --no-host --steps 10 --warmup 3"
+tools/gpu_session.sh \
+ "pp_tests::300::python -u -m pytest tests/test_gpu_pp.py -x -v --timeout 120 --timeout-method thread" \
+ "ppA::120::$B --workload A --pp" \
+ "ppB::120::$B --workload B --pp" \
+ "D_d6::200::$B --workload D" \
+ "D_d12::200::$B --workload D --opt tile_depth=12"
