@@ -380,6 +380,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check recovered data after timing")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) leg")
+    ap.add_argument("--loss-mode", choices=("random", "fixed"), default="random",
+                    help="lost data rows: a fresh random set per group, or rows 0..r-1 in every "
+                         "group")
+    ap.add_argument("--parity", choices=("random", "first"), default="random",
+                    help="parity rows received: a random r-subset per group, or the first r")
     ap.add_argument("--pp", action="store_true",
                     help="also time the packet-protection step (encode + NullEncrypter seal of "
                          "the FEC packets, open)")
@@ -450,8 +455,8 @@ def main():
     parity = torch.zeros((G, m, bb), dtype=torch.uint8, device=dev)
     rc = eng.encode(k, m, bb, data, parity)
     assert rc == 0, rc
-    rows_np, src_np = synth.loss_patterns(k, m, r, G, shard.loss_seed(seed, rank), mode="random",
-                                          parity="random", shuffle=False)
+    rows_np, src_np = synth.loss_patterns(k, m, r, G, shard.loss_seed(seed, rank),
+                                          mode=args.loss_mode, parity=args.parity, shuffle=False)
     rows = torch.from_numpy(rows_np).to(dev)
     src = torch.from_numpy(src_np).to(dev)
     blocks = torch.empty((G, k, bb), dtype=torch.uint8, device=dev)
@@ -605,7 +610,8 @@ def main():
                 "k": k, "m": m, "payload_bytes": payload, "block_bytes": bb,
                 "losses_per_group": r,
                 "parallelism": f"{world} independent group shards (no collective)",
-                "decode_layout": args.decode_layout,
+                "decode_layout": args.decode_layout, "loss_mode": args.loss_mode,
+                "parity_rows": args.parity,
                 "options": args.opt,
             },
             "roofline": {
