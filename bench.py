@@ -477,36 +477,62 @@ def main():
 
     def step(i=None):
         if i is not None:
-            rec(3 * i)
+            rec(4 * i, 4 * i + 1)
         eng.encode(k, m, bb, data, parity)
         kernels["encode"] = fec.last_kernels()
         if i is not None:
-            rec(3 * i + 1)
+            rec(4 * i + 2, 4 * i + 3)
         if recovered:
             eng.decode_recovered(k, m, bb, blocks, rows, out, rows_out, status=status)
         else:
             eng.decode(k, m, bb, blocks, rows, out=out, rows_out=rows_out, status=status)
         kernels["decode"] = fec.last_kernels()
         if i is not None:
-            rec(3 * i + 2)
+            rec(None, None)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
 
     # ---- timed region: barrier + sync on both sides, K steps
-    # per-kernel HIP events on the launch stream: device-scope release when the runtime
-    # offers it (DeviceEvents), torch's default events otherwise
+    # Per-phase kernel timing with HIP events on the launch stream.  The library records a
+    # start event at its first kernel's start and a stop event at its last kernel's end
+    # (qfec_set_timing_events -> hipExtLaunchKernel), so a phase is timed from its kernels
+    # alone, as rocprofv3 times them.  Fallback: event pairs recorded between the calls
+    # (these also count the dispatch gaps, ~5-10 us per launch).
+    from quic_amd import _lib
+    lib = _lib.load()
     try:
-        dev_ev = DeviceEvents(3 * args.steps)
-        event_kind = "hipEventReleaseToDevice"
-        rec = lambda j: dev_ev.record(j, stream)
+        dev_ev = DeviceEvents(4 * args.steps)
+        event_kind = "hipExtLaunchKernel start/stop events"
+
+        def rec(a, b):
+            ea = dev_ev.ev[a] if a is not None else None
+            eb = dev_ev.ev[b] if b is not None else None
+            if lib.qfec_set_timing_events(ea, eb) != 0:
+                raise RuntimeError("qfec_set_timing_events failed")
         elapsed_ev = dev_ev.elapsed_ms
+        # probe once outside the timed region: both events must have been recorded
+        rec(0, 1)
+        eng.encode(k, m, bb, data, parity)
+        rec(None, None)
+        torch.cuda.synchronize(dev)
+        if not elapsed_ev(0, 1) > 0:
+            raise RuntimeError("kernel events not recorded")
     except Exception:
+        if lib.qfec_set_timing_events(None, None) != 0:
+            raise
         dev_ev = None
-        event_kind = "torch.cuda.Event"
-        tev = [torch.cuda.Event(enable_timing=True) for _ in range(3 * args.steps)]
-        rec = lambda j: tev[j].record(stream)
+        event_kind = "torch.cuda.Event pairs between calls"
+        tev = [torch.cuda.Event(enable_timing=True) for _ in range(4 * args.steps)]
+        pending = [None]   # stop event of the phase in progress
+
+        def rec(a, b):
+            if pending[0] is not None:
+                tev[pending[0]].record(stream)
+            if a is not None:
+                tev[a].record(stream)
+            pending[0] = b
         elapsed_ev = lambda a, b: tev[a].elapsed_time(tev[b])
     if world > 1:
         dist.barrier()
@@ -518,8 +544,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    enc_ms = float(np.mean([elapsed_ev(3 * i, 3 * i + 1) for i in range(args.steps)]))
-    dec_ms = float(np.mean([elapsed_ev(3 * i + 1, 3 * i + 2) for i in range(args.steps)]))
+    enc_ms = float(np.mean([elapsed_ev(4 * i, 4 * i + 1) for i in range(args.steps)]))
+    dec_ms = float(np.mean([elapsed_ev(4 * i + 2, 4 * i + 3) for i in range(args.steps)]))
     if dev_ev is not None:
         dev_ev.close()
 
@@ -626,7 +652,7 @@ def main():
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": dom[2],
                 "launch_ms": round(dom[3], 5),
-                "timing": event_kind + " pairs around each launch, launch stream, timed steps",
+                "timing": event_kind + " on the launch stream, per phase, timed steps",
             },
             "kernels": {
                 "encode": kernels["encode"], "decode": kernels["decode"],

@@ -200,6 +200,11 @@ QFEC_API const char *qfec_last_error(void);
 /* Names of the kernels this thread's last engine call launched, " + "-separated, e.g.
  * "decode_prep_lane_kernel + gf_stream_kernel<decode>" (bench.py reports it). */
 QFEC_API const char *qfec_last_kernels(void);
+/* Measurement hook (bench.py's roofline timing).  While set, every engine call on this
+ * thread records start_event (a hipEvent_t) at the start of its first kernel and
+ * stop_event at the end of its last, through hipExtLaunchKernel, so the pair brackets the
+ * call's kernels only.  Pass NULL, NULL to stop.  Returns -2 if only one is NULL. */
+QFEC_API int qfec_set_timing_events(void *start_event, void *stop_event);
 QFEC_API int qfec_version(void);
 
 #ifdef __cplusplus

@@ -158,6 +158,7 @@ namespace {
 
 int set_device(qfec_ctx* c) {
     g_kernels.clear();
+    qfec::launch_timing().first = true;
     QF_HIP(hipSetDevice(c->device));
     return 0;
 }
@@ -482,6 +483,11 @@ int default_ctx(qfec_ctx** out) {
 }  // namespace
 
 namespace qfec {
+LaunchTiming& launch_timing() {
+    static thread_local LaunchTiming t;
+    return t;
+}
+
 void note_kernel(const char* name) {
     // a host-pointer batch launches the same kernels once per chunk: list each once
     const std::string n(name);
@@ -506,6 +512,15 @@ int qfec_version(void) { return 1; }
 const char* qfec_last_error(void) { return g_err.c_str(); }
 
 const char* qfec_last_kernels(void) { return g_kernels.c_str(); }
+
+int qfec_set_timing_events(void* start_event, void* stop_event) {
+    if (!start_event != !stop_event) return fail(-2, "set both timing events or neither");
+    qfec::LaunchTiming& t = qfec::launch_timing();
+    t.start = (hipEvent_t)start_event;
+    t.stop = (hipEvent_t)stop_event;
+    t.first = true;
+    return 0;
+}
 
 int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
     if (!c || !name) return fail(-2, "null context or option name");

@@ -7,6 +7,7 @@
 //   rows     [G][k]       row tag of each received block (data 0..k-1, parity k..k+m-1)
 // The bit-sliced code treats every block as 8 sub-rows of s bytes; see DESIGN.md.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -37,6 +38,29 @@ struct Tune {
 
 // Records the name of a kernel a call launched (qfec_last_kernels(), per thread).
 void note_kernel(const char* name);
+
+// Kernel timing hook (qfec_set_timing_events, per thread).  While a stop event is set, each
+// engine call records `start` at the start of its first kernel and `stop` at the end of
+// every kernel (the last record wins), through hipExtLaunchKernel: the events bracket the
+// kernels themselves, not the launch gaps around them, so they agree with rocprofv3.
+struct LaunchTiming {
+    hipEvent_t start = nullptr, stop = nullptr;
+    bool first = true;   // the call's first kernel has not been launched yet
+};
+LaunchTiming& launch_timing();
+
+// Every kernel of the library is launched through this.
+template <typename F, typename... Args>
+inline void qlaunch(F kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st,
+                    Args... args) {
+    LaunchTiming& t = launch_timing();
+    hipEvent_t a = nullptr;
+    if (t.stop && t.first) {
+        a = t.start;
+        t.first = false;
+    }
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, st, a, t.stop, 0u, args...);
+}
 
 // Decode work tables written by the prep kernel and read by the apply kernel.
 struct DecodeWork {

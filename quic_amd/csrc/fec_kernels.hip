@@ -926,9 +926,9 @@ static void xor_flat_launch(const uint8_t* in, uint8_t* out, const uint8_t* eidx
     const unsigned total = (unsigned)(G * nu);
     const unsigned nb = (total + 255) / 256;
     switch (k) {
-        case 10: xor_flat_kernel<VS, 10, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs, es); break;
-        case 32: xor_flat_kernel<VS, 32, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs, es); break;
-        default: xor_flat_kernel<VS, 0, DECODE><<<nb, 256, 0, st>>>(in, out, eidx, k, bb, nu, total, igs, ogs, es); break;
+        case 10: qlaunch((xor_flat_kernel<VS, 10, DECODE>), dim3(nb), dim3(256), 0, st, in, out, eidx, k, bb, nu, total, igs, ogs, es); break;
+        case 32: qlaunch((xor_flat_kernel<VS, 32, DECODE>), dim3(nb), dim3(256), 0, st, in, out, eidx, k, bb, nu, total, igs, ogs, es); break;
+        default: qlaunch((xor_flat_kernel<VS, 0, DECODE>), dim3(nb), dim3(256), 0, st, in, out, eidx, k, bb, nu, total, igs, ogs, es); break;
     }
 }
 
@@ -947,7 +947,7 @@ static hipError_t xor_any(const uint8_t* in, uint8_t* out, const uint8_t* eidx, 
     if (units > 0xffffffffLL) return hipErrorInvalidValue;
     if (vs == 16) xor_flat_launch<16, DECODE>(in, out, eidx, k, bb, G, igs, ogs, st, es);
     else if (vs == 4) xor_flat_launch<4, DECODE>(in, out, eidx, k, bb, G, igs, ogs, st, es);
-    else xor_bytes_kernel<DECODE><<<(unsigned)((units + 255) / 256), 256, 0, st>>>(in, out, eidx, k, bb, units, igs, ogs, es);
+    else qlaunch((xor_bytes_kernel<DECODE>), dim3((unsigned)((units + 255) / 256)), dim3(256), 0, st, in, out, eidx, k, bb, units, igs, ogs, es);
     return hipGetLastError();
 }
 
@@ -969,7 +969,7 @@ hipError_t launch_xor_decode(const uint8_t* blocks, uint8_t* out, const uint8_t*
         return launch_xor_dma(blocks, out, nullptr, rows_in, rows_out, status, k, bb, groups, ogs,
                               true, st, t, compact);
     note_kernel("m1_prep_kernel");
-    m1_prep_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(rows_in, rows_out, status,
+    qlaunch((m1_prep_kernel), dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, rows_in, rows_out, status,
                                                                      eidx, k, groups,
                                                                      compact ? 1 : 0);
     hipError_t e = hipGetLastError();
@@ -983,7 +983,7 @@ hipError_t launch_replicate(const uint8_t* data, uint8_t* parity, int m, int bb,
     const long long total = groups * m * (long long)bb;
     const unsigned nb = (unsigned)std::min<long long>((total + 255) / 256, 65536);
     note_kernel("replicate_kernel");
-    replicate_kernel<<<nb, 256, 0, st>>>(data, parity, m, bb, groups);
+    qlaunch((replicate_kernel), dim3(nb), dim3(256), 0, st, data, parity, m, bb, groups);
     return hipGetLastError();
 }
 
@@ -994,7 +994,7 @@ hipError_t launch_rec_k1(const uint8_t* blocks, const uint8_t* rows_in, uint8_t*
     const long long total = groups * (long long)bb;
     const unsigned nb = (unsigned)std::min<long long>((total + 255) / 256, 65536);
     note_kernel("rec_k1_kernel");
-    rec_k1_kernel<<<nb, 256, 0, st>>>(blocks, rows_in, rec, rec_rows, status, bb, rmax, groups);
+    qlaunch((rec_k1_kernel), dim3(nb), dim3(256), 0, st, blocks, rows_in, rec, rec_rows, status, bb, rmax, groups);
     return hipGetLastError();
 }
 
@@ -1002,7 +1002,7 @@ hipError_t launch_rows_k1(const uint8_t* rows_in, uint8_t* rows_out, int32_t* st
                           long long groups, hipStream_t st) {
     if (groups <= 0) return hipSuccess;
     note_kernel("rows_k1_kernel");
-    rows_k1_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, st>>>(rows_in, rows_out, status,
+    qlaunch((rows_k1_kernel), dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, rows_in, rows_out, status,
                                                                      groups);
     return hipGetLastError();
 }
@@ -1034,15 +1034,15 @@ static hipError_t gf_apply_dispatch(const uint8_t* in, uint8_t* out, const uint8
     do {                                                                                      \
         if (flat) {                                                                           \
             if constexpr (!DECODE)                                                            \
-                gf_apply_kernel<RCV, false, false, 2, true><<<nb, nthr, 0, st>>>(QF_ARGS);    \
+                qlaunch((gf_apply_kernel<RCV, false, false, 2, true>), dim3(nb), dim3(nthr), 0, st, QF_ARGS);    \
         } else if (s >= 4 && pd == 3)                                                         \
-            gf_apply_kernel<RCV, DECODE, false, 3><<<nb, nthr, 0, st>>>(QF_ARGS);             \
+            qlaunch((gf_apply_kernel<RCV, DECODE, false, 3>), dim3(nb), dim3(nthr), 0, st, QF_ARGS);             \
         else if (s >= 4 && pd == 1)                                                           \
-            gf_apply_kernel<RCV, DECODE, false, 1><<<nb, nthr, 0, st>>>(QF_ARGS);             \
+            qlaunch((gf_apply_kernel<RCV, DECODE, false, 1>), dim3(nb), dim3(nthr), 0, st, QF_ARGS);             \
         else if (s >= 4)                                                                      \
-            gf_apply_kernel<RCV, DECODE, false, 2><<<nb, nthr, 0, st>>>(QF_ARGS);             \
+            qlaunch((gf_apply_kernel<RCV, DECODE, false, 2>), dim3(nb), dim3(nthr), 0, st, QF_ARGS);             \
         else                                                                                  \
-            gf_apply_kernel<RCV, DECODE, true, 1><<<nb, nthr, 0, st>>>(QF_ARGS);              \
+            qlaunch((gf_apply_kernel<RCV, DECODE, true, 1>), dim3(nb), dim3(nthr), 0, st, QF_ARGS);              \
     } while (0)
     switch (rc) {
         case 1: QF_LAUNCH(1); break;
@@ -1079,7 +1079,7 @@ hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t
         const size_t lds = (((size_t)m * k + 15) & ~(size_t)15) + 64 * (size_t)k +
                            64 * (size_t)(k + 1) * 4;
         note_kernel("decode_prep_lane_kernel");
-        decode_prep_lane_kernel<<<nb, 256, lds, st>>>(
+        qlaunch((decode_prep_lane_kernel), dim3(nb), dim3(256), lds, st, 
             rows_in, rows_out, status, cenc, w.coef, w.slots, w.nout, rec_rows, groups, k, m, bb,
             rmax);
         return hipGetLastError();
@@ -1093,7 +1093,7 @@ hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t
     const long long want = (groups + nwv - 1) / nwv;
     const unsigned nb = (unsigned)std::min<long long>(want, (long long)t.cus * 16);
     note_kernel(syndrome ? "decode_prep_kernel<syndrome>" : "decode_prep_kernel");
-    decode_prep_kernel<<<nb, nwv * 64, lds, st>>>(rows_in, rows_out, status, cenc, w.coef,
+    qlaunch((decode_prep_kernel), dim3(nb), dim3(nwv * 64), lds, st, rows_in, rows_out, status, cenc, w.coef,
                                                    w.slots, w.nout, rec_rows, groups, k, m, bb,
                                                    rc, rmax, nchunk, scratch, syndrome ? 1 : 0);
     return hipGetLastError();
@@ -1114,7 +1114,7 @@ hipError_t launch_scatter_recovered(const uint8_t* scratch, uint8_t* out, Decode
     const long long units = groups * rmax;
     if (units <= 0) return hipSuccess;
     note_kernel("scatter_recovered_kernel");
-    scatter_recovered_kernel<<<blocks_for_waves(units), 256, 0, st>>>(scratch, out, w.slots,
+    qlaunch((scatter_recovered_kernel), dim3(blocks_for_waves(units)), dim3(256), 0, st, scratch, out, w.slots,
                                                                       w.nout, k, bb, rmax,
                                                                       units);
     return hipGetLastError();
@@ -1136,7 +1136,7 @@ hipError_t launch_synth_fill(uint8_t* dst, unsigned long long bytes, unsigned lo
     if (byte_offset % 8) return hipErrorInvalidValue;
     const unsigned long long words = bytes / 8 + 1;
     const unsigned nb = (unsigned)std::min<unsigned long long>((words + 255) / 256, 1u << 16);
-    synth_fill_kernel<<<nb, 256, 0, st>>>(dst, bytes, seed, byte_offset);
+    qlaunch((synth_fill_kernel), dim3(nb), dim3(256), 0, st, dst, bytes, seed, byte_offset);
     return hipGetLastError();
 }
 
@@ -1145,7 +1145,7 @@ hipError_t launch_synth_gather(const uint8_t* data, const uint8_t* parity, const
                                hipStream_t st) {
     const long long units = groups * k;
     if (units <= 0) return hipSuccess;
-    synth_gather_kernel<<<blocks_for_waves(units), 256, 0, st>>>(data, parity, src, blocks, k,
+    qlaunch((synth_gather_kernel), dim3(blocks_for_waves(units)), dim3(256), 0, st, data, parity, src, blocks, k,
                                                                  m, bb, units);
     return hipGetLastError();
 }

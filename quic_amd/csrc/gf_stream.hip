@@ -648,7 +648,7 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     const unsigned threads = kStreamWaves * 64;
     const int s = bb / 8;
 #define QS_GO(RCV, SV, DEC, RCPV, KCV)                                                        \
-    hipLaunchKernelGGL((gf_stream_kernel<RCV, SV, DEC, RCPV, KCV>), dim3(grid), dim3(threads), \
+    qlaunch((gf_stream_kernel<RCV, SV, DEC, RCPV, KCV>), dim3(grid), dim3(threads), \
                        lds, st, in, out, coef, slots, nout, groups, k, m, rmax, coef_gstride,   \
                        out_gstride, R, s)
 #define QS_DEC(SV)                                        \
@@ -680,7 +680,7 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         if (t.stream_grid > 0) rcap = t.stream_grid;
         const unsigned rgrid = (unsigned)std::min<long long>(rwant, rcap);
 #define QR_GO(RCV, DEC, MCV)                                                                   \
-    hipLaunchKernelGGL((gf_ring_kernel<32, 169, RCV, DEC, MCV>), dim3(rgrid),                   \
+    qlaunch((gf_ring_kernel<32, 169, RCV, DEC, MCV>), dim3(rgrid),                   \
                        dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax, \
                        coef_gstride, out_gstride)
         note_kernel("gf_ring_kernel<encode,k32m4>");

@@ -646,10 +646,10 @@ hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, 
     const unsigned grid = (unsigned)std::min<long long>(groups, cap);
     note_kernel("gf_tile_kernel<encode,k128m16>");
     if (t.tile_depth == 12)
-        hipLaunchKernelGGL((gf_tile_kernel<kTileS, 8, nch, 12, 128, 16>), dim3(grid), dim3(threads),
+        qlaunch((gf_tile_kernel<kTileS, 8, nch, 12, 128, 16>), dim3(grid), dim3(threads),
                            lds, st, in, out, groups, out_gstride);
     else
-        hipLaunchKernelGGL((gf_tile_kernel<kTileS, 8, nch, 6, 128, 16>), dim3(grid), dim3(threads),
+        qlaunch((gf_tile_kernel<kTileS, 8, nch, 6, 128, 16>), dim3(grid), dim3(threads),
                            lds, st, in, out, groups, out_gstride);
     return hipGetLastError();
 }
@@ -677,7 +677,7 @@ hipError_t launch_gf_tile_syndrome(const uint8_t* in, uint8_t* out, const uint8_
     if (t.tile_grid > 0) cap = t.tile_grid;
     const unsigned grid = (unsigned)std::min<long long>(groups, cap);
     note_kernel("gf_tile_syn_kernel<decode,k128m16>");
-    hipLaunchKernelGGL((gf_tile_syn_kernel<kTileS, D>), dim3(grid), dim3(threads), lds, st, in,
+    qlaunch((gf_tile_syn_kernel<kTileS, D>), dim3(grid), dim3(threads), lds, st, in,
                        out, tab, slots, nout, cenc, groups, rmax, tab_gstride, out_gstride);
     return hipGetLastError();
 }

@@ -221,7 +221,7 @@ hipError_t launch_null_seal(long long n, const uint8_t* ad, long long ad_stride,
     if ((((uintptr_t)out) | (uintptr_t)out_stride) & 3) return hipErrorInvalidValue;
     if (pp_grid(n) > 0x7fffffffu) return hipErrorInvalidValue;
     note_kernel("null_seal_kernel");
-    hipLaunchKernelGGL(null_seal_kernel, dim3(pp_grid(n)), dim3(kPPWaves * 64), 0, st, n, ad,
+    qlaunch(null_seal_kernel, dim3(pp_grid(n)), dim3(kPPWaves * 64), 0, st, n, ad,
                        ad_stride, ad_len, ad_all, pt, pt_stride, pt_len, pt_all, out, out_stride,
                        out_len);
     return hipGetLastError();
@@ -235,7 +235,7 @@ hipError_t launch_null_open(long long n, const uint8_t* pkt, long long pkt_strid
     if ((((uintptr_t)out) | (uintptr_t)out_stride) & 3) return hipErrorInvalidValue;
     if (pp_grid(n) > 0x7fffffffu) return hipErrorInvalidValue;
     note_kernel("null_open_kernel");
-    hipLaunchKernelGGL(null_open_kernel, dim3(pp_grid(n)), dim3(kPPWaves * 64), 0, st, n, pkt,
+    qlaunch(null_open_kernel, dim3(pp_grid(n)), dim3(kPPWaves * 64), 0, st, n, pkt,
                        pkt_stride, pkt_len, pkt_all, ad_len, ad_all, out, out_stride, out_len);
     return hipGetLastError();
 }

@@ -209,7 +209,7 @@ hipError_t xor_go(const XorPlan& p, const uint8_t* in, uint8_t* out, const uint8
         note_kernel(DECODE ? (COMPACT ? "xor_dma_kernel<decode,recovered>"
                                       : "xor_dma_kernel<decode>")
                            : "xor_dma_kernel<encode>");
-        xor_dma_kernel<N, NSLOT, DECODE, FUSED, 0, COMPACT><<<nb, p.waves * 64, p.lds, st>>>(
+        qlaunch((xor_dma_kernel<N, NSLOT, DECODE, FUSED, 0, COMPACT>), dim3(nb), dim3(p.waves * 64), p.lds, st, 
             in, out, eidx, rows_in, rows_out, status, k, bb, G, ogs);
         return hipGetLastError();
     }
