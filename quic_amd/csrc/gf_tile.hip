@@ -110,16 +110,19 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
     constexpr int k = KC;
     const long long G0 = blockIdx.x, GS = gridDim.x;
     if (G0 >= groups) return;                        // uniform over the workgroup
-    const long long cnt = (groups - 1 - G0) / GS + 1;
-    const long long nblocks = cnt * k;               // this workgroup's block stream
+    // wave-uniform 32-bit stream counters, in SGPRs (the launcher checks cnt * k < 2^31):
+    // 64-bit or VGPR-resident counters cost a VALU compare and a branch per block
+    const int cnt = __builtin_amdgcn_readfirstlane((int)((groups - 1 - G0) / GS + 1));
+    const int nblocks = cnt * k;                     // this workgroup's block stream
 
-    // ---- DMA side: block b of the stream = block iss_x of group G0 + iss_i * GS
-    long long iss_b = 0;
+    // ---- DMA side: block b of the stream = block iss_x of group G0 + iss_i * GS, into
+    // ring buffer iss_slot = b mod NBUF
+    int iss_slot = 0;
     int iss_x = 0;
     const uint8_t* iss_src = in + G0 * (long long)k * BB;
     const long long gstride = GS * (long long)k * BB;
     auto issue_next = [&]() {
-        uint8_t* dst = smem + (int)(iss_b % NBUF) * BBP;
+        uint8_t* dst = smem + iss_slot * BBP;
         const uint8_t* src = iss_src + (long long)iss_x * BB;
 #pragma unroll
         for (int q = 0; q < PPW; ++q) {
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
             __builtin_amdgcn_global_load_lds(QT_GPTR(src + off), QT_LPTR(dst + p * 1024), 16, 0,
                                              2);
         }
-        ++iss_b;
+        if (++iss_slot == NBUF) iss_slot = 0;
         if (++iss_x == k) {
             iss_x = 0;
             iss_src += gstride;
@@ -137,10 +140,10 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
 
     // ---- LDS side: column word c of the 8 sub-rows of block b (aligned dwords; sub-row t
     // starts t * S bytes into the buffer, misaligned by (t * S) & 3, realigned at use)
-    auto read_block = [&](long long b, uint32_t (&lo)[8], uint32_t (&hi)[8]) {
+    auto read_block = [&](int b, uint32_t (&lo)[8], uint32_t (&hi)[8]) {
         uint32_t c4 = 4u * (uint32_t)c;
         asm volatile("" : "+v"(c4));   // no hoisting across blocks
-        const uint8_t* L = smem + (int)(b % NBUF) * BBP + c4;
+        const uint8_t* L = smem + (int)((unsigned)b % NBUF) * BBP + c4;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const int o = t * S;
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
         }
     };
     // wait for block bw's pieces (this wave's), then for every wave's
-    auto wait_block = [&](long long bw, bool after_stores) {
+    auto wait_block = [&](int bw, bool after_stores) {
         if (bw + AHEAD < nblocks) {
             if (after_stores) tile_wait_vmcnt<WAITG>();
             else tile_wait_vmcnt<WAITN>();
@@ -167,9 +170,9 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
     wait_block(0, false);
     read_block(0, lo0, hi0);
 
-    long long b = 0;   // stream index of the current block
+    int b = 0;   // stream index of the current block
 #pragma unroll 1
-    for (long long i = 0; i < cnt; ++i) {
+    for (int i = 0; i < cnt; ++i) {
         const long long g = G0 + i * GS;
         const int n = min(MC - chunk * RC, RC);      // chunk h owns outputs h * RC + j
         uint32_t acc[RC][8];
@@ -312,17 +315,17 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
     const int c = min(tile * 64 + lane, NW - 1);
     const long long G0 = blockIdx.x, GS = gridDim.x;
     if (G0 >= groups) return;
-    const long long cnt = (groups - 1 - G0) / GS + 1;
-    const long long nblocks = cnt * KC;
+    const int cnt = __builtin_amdgcn_readfirstlane((int)((groups - 1 - G0) / GS + 1));
+    const int nblocks = cnt * KC;                    // 32-bit, in SGPRs (see gf_tile_kernel)
 
     // ---- DMA side: stream block x of group G0 + i * GS = its slot perm[x]
-    long long iss_b = 0;
+    int iss_slot = 0;
     int iss_x = 0;
     const uint8_t* iss_src = in + G0 * (long long)KC * BB;
     const uint8_t* iss_tab = tab + G0 * tab_gstride;
     const long long gstride = GS * (long long)KC * BB;
     auto issue_next = [&]() __attribute__((always_inline)) {
-        uint8_t* dst = smem + (int)(iss_b % NBUF) * BBP;
+        uint8_t* dst = smem + iss_slot * BBP;
         const int slot = min(tile_cload_u8(iss_tab + syn::kPerm, iss_x), KC - 1);
         const uint8_t* src = iss_src + (long long)slot * BB;
 #pragma unroll
@@ -332,18 +335,18 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
             __builtin_amdgcn_global_load_lds(QT_GPTR(src + off), QT_LPTR(dst + p * 1024), 16, 0,
                                              2);
         }
-        ++iss_b;
+        if (++iss_slot == NBUF) iss_slot = 0;
         if (++iss_x == KC) {
             iss_x = 0;
             iss_src += gstride;
             iss_tab += GS * tab_gstride;
         }
     };
-    auto read_block = [&](long long bi, uint32_t (&lo)[8], uint32_t (&hi)[8])
+    auto read_block = [&](int bi, uint32_t (&lo)[8], uint32_t (&hi)[8])
                           __attribute__((always_inline)) {
         uint32_t c4 = 4u * (uint32_t)c;
         asm volatile("" : "+v"(c4));   // no hoisting across blocks
-        const uint8_t* L = smem + (int)(bi % NBUF) * BBP + c4;
+        const uint8_t* L = smem + (int)((unsigned)bi % NBUF) * BBP + c4;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const int o = t * S;
@@ -352,7 +355,7 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
             hi[t] = (o & 3) ? q[1] : 0u;
         }
     };
-    auto wait_block = [&](long long bw, bool after_stores) __attribute__((always_inline)) {
+    auto wait_block = [&](int bw, bool after_stores) __attribute__((always_inline)) {
         if (bw + AHEAD < nblocks) {
             if (after_stores) tile_wait_vmcnt<WAITG>();
             else tile_wait_vmcnt<WAITN>();
@@ -369,9 +372,9 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
     wait_block(0, false);
     read_block(0, lo0, hi0);
 
-    long long b = 0;
+    int b = 0;
 #pragma unroll 1
-    for (long long i = 0; i < cnt; ++i) {
+    for (int i = 0; i < cnt; ++i) {
         const long long g = G0 + i * GS;
         const uint8_t* tb = tab + g * tab_gstride;
         uint32_t pm[4];
@@ -395,7 +398,7 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
             if (b + 1 < nblocks) {
                 // positions 0 .. D - 1 of a group were DMA'd before the previous group's
                 // stores were issued, so those stores are younger than their pieces
-                const long long p1 = b + 1 - i * KC;
+                const int p1 = b + 1 - i * KC;
                 wait_block(b + 1, i > 0 && p1 <= D - 1);
                 read_block(b + 1, nlo, nhi);
             }
@@ -644,6 +647,7 @@ hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, 
     long long cap = (long long)t.cus * per_cu;
     if (t.tile_grid > 0) cap = t.tile_grid;              // tests: many groups per workgroup
     const unsigned grid = (unsigned)std::min<long long>(groups, cap);
+    if ((groups + grid - 1) / grid * k >= (1LL << 31)) return hipErrorInvalidValue;
     note_kernel("gf_tile_kernel<encode,k128m16>");
     if (t.tile_depth == 12)
         qlaunch((gf_tile_kernel<kTileS, 8, nch, 12, 128, 16>), dim3(grid), dim3(threads),
@@ -676,6 +680,7 @@ hipError_t launch_gf_tile_syndrome(const uint8_t* in, uint8_t* out, const uint8_
     long long cap = (long long)t.cus * std::max(1, (int)((160 * 1024) / lds));
     if (t.tile_grid > 0) cap = t.tile_grid;
     const unsigned grid = (unsigned)std::min<long long>(groups, cap);
+    if ((groups + grid - 1) / grid * k >= (1LL << 31)) return hipErrorInvalidValue;
     note_kernel("gf_tile_syn_kernel<decode,k128m16>");
     qlaunch((gf_tile_syn_kernel<kTileS, D>), dim3(grid), dim3(threads), lds, st, in,
                        out, tab, slots, nout, cenc, groups, rmax, tab_gstride, out_gstride);

@@ -85,3 +85,13 @@ def test_no_environment_knobs_in_product():
     out = subprocess.run(["strings", _lib.LIB_PATH], capture_output=True, text=True).stdout
     names = set(re.findall(r"\bQFEC_[A-Z0-9_]+", out))
     assert names <= {"QFEC_DEVICE"}, names
+
+
+def test_timing_events_hook_arguments():
+    # qfec_set_timing_events: both events or neither (no GPU call is made)
+    import ctypes
+    L = _lib.load()
+    assert L.qfec_set_timing_events(None, None) == 0
+    assert L.qfec_set_timing_events(ctypes.c_void_p(1), None) == -2
+    assert L.qfec_set_timing_events(None, ctypes.c_void_p(1)) == -2
+    assert L.qfec_set_timing_events(None, None) == 0
