@@ -533,7 +533,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
         {"const_enc", &t.const_enc, 0, 1},     {"tile", &t.tile, 0, 1},
         {"stream_static", &t.stream_static, 0, 1},
-        {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_depth", &t.tile_depth, 6, 12},
+        {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_depth", &t.tile_depth, 4, 6},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -541,7 +541,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
     for (const Opt& o : opts) {
         if (strcmp(o.n, name) != 0) continue;
         if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))) ||
-            (o.p == &t.tile_depth && value != 6 && value != 12))
+            (o.p == &t.tile_depth && value != 4 && value != 6))
             return fail(-2, std::string("option value out of range: ") + name);
         *o.p = value;
         return 0;

@@ -637,7 +637,7 @@ hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, 
     if (groups <= 0) return hipSuccess;
     if (!gf_tile_supported(k, m, bb, t)) return hipErrorInvalidValue;
     if (((uintptr_t)in & 15) != 0) return hipErrorInvalidValue;
-    if (t.tile_depth != 6 && t.tile_depth != 12) return hipErrorInvalidValue;
+    if (t.tile_depth != 4 && t.tile_depth != 6) return hipErrorInvalidValue;
     using TS = TileShape<kTileS>;
     constexpr int nch = 2;
     const size_t lds = (size_t)(t.tile_depth + 2) * TS::BBP;
@@ -649,8 +649,8 @@ hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, 
     const unsigned grid = (unsigned)std::min<long long>(groups, cap);
     if ((groups + grid - 1) / grid * k >= (1LL << 31)) return hipErrorInvalidValue;
     note_kernel("gf_tile_kernel<encode,k128m16>");
-    if (t.tile_depth == 12)
-        qlaunch((gf_tile_kernel<kTileS, 8, nch, 12, 128, 16>), dim3(grid), dim3(threads),
+    if (t.tile_depth == 4)
+        qlaunch((gf_tile_kernel<kTileS, 8, nch, 4, 128, 16>), dim3(grid), dim3(threads),
                            lds, st, in, out, groups, out_gstride);
     else
         qlaunch((gf_tile_kernel<kTileS, 8, nch, 6, 128, 16>), dim3(grid), dim3(threads),

@@ -394,7 +394,7 @@ OPTION_SETS = [
     {"dma": 0}, {"stream": 0}, {"stream": 0, "pd": 1}, {"stream": 0, "pd": 3},
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
     {"stream_ring": 36}, {"host_chunk_mb": 1}, {"const_enc": 0}, {"tile": 0},
-    {"tile_depth": 12}, {"stream_static": 0},
+    {"tile_depth": 4}, {"stream_static": 0},
 ]
 
 
@@ -612,7 +612,7 @@ def test_stream_any_small_block(engine, oracle, bb, k, m, r):
 
 
 # ------------------------------------------------- gf_tile (9008-byte blocks, config D)
-@pytest.mark.parametrize("depth", [6, 12])
+@pytest.mark.parametrize("depth", [4, 6])
 @pytest.mark.parametrize("grid", [1, 3, 0])
 @pytest.mark.parametrize("k,m,r", [(128, 16, 8), (128, 16, 13), (40, 16, 16), (16, 6, 4)])
 def test_tile_many_groups_per_workgroup(tuned_engine, oracle, depth, grid, k, m, r):
