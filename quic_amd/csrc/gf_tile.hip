@@ -324,9 +324,14 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
     const uint8_t* iss_src = in + G0 * (long long)KC * BB;
     const uint8_t* iss_tab = tab + G0 * tab_gstride;
     const long long gstride = GS * (long long)KC * BB;
+    // the stream-order bytes come 4 at a time: one scalar load (and its lgkmcnt wait) per
+    // four issued blocks instead of one per block (KC % 4 == 0: a word never spans groups)
+    uint32_t perm_w = 0;
+    static_assert(KC % 4 == 0 && syn::kPerm % 4 == 0, "stream-order words");
     auto issue_next = [&]() __attribute__((always_inline)) {
         uint8_t* dst = smem + iss_slot * BBP;
-        const int slot = min(tile_cload_u8(iss_tab + syn::kPerm, iss_x), KC - 1);
+        if ((iss_x & 3) == 0) perm_w = tile_cload_u32(iss_tab, syn::kPerm + iss_x);
+        const int slot = min((int)((perm_w >> (8 * (iss_x & 3))) & 0xFFu), KC - 1);
         const uint8_t* src = iss_src + (long long)slot * BB;
 #pragma unroll
         for (int q = 0; q < PPW; ++q) {
