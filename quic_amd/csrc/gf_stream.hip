@@ -104,7 +104,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const long long W = (long long)gridDim.x * kStreamWaves;
     const long long g0 = (long long)blockIdx.x * kStreamWaves + w;
     if (g0 >= groups) return;
-    const long long cnt = (groups - 1 - g0) / W + 1;   // groups of this wave
+    const long long cnt =   // wave-uniform, kept in SGPRs (the division runs on the VALU)
+        __builtin_amdgcn_readfirstlane((int)((groups - 1 - g0) / W + 1));   // groups of this wave
     if constexpr (KC > 0) k = KC;
     const int gb = k * BB;
     const int NP = (gb + 1023) >> 10;                  // pieces per group
@@ -387,7 +388,8 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
     const long long W = (long long)gridDim.x * kRingWaves;
     const long long g0 = (long long)blockIdx.x * kRingWaves + w;
     if (g0 >= groups) return;
-    const long long cnt = (groups - 1 - g0) / W + 1;      // groups of this wave
+    const long long cnt =   // wave-uniform, kept in SGPRs (the division runs on the VALU)
+        __builtin_amdgcn_readfirstlane((int)((groups - 1 - g0) / W + 1));      // groups of this wave
     const int c = lane < NW ? lane : NW - 1;              // idle lanes shadow the last word
     const long long gstep = W * GB;
 

@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) void xor_dma_kernel(
     const long long W = (long long)gridDim.x * nwv;
     const long long g0 = (long long)blockIdx.x * nwv + w;
     if (g0 >= groups) return;
-    const long long cnt = (groups - 1 - g0) / W + 1;   // groups of this wave
+    const long long cnt =   // wave-uniform, kept in SGPRs (the division runs on the VALU)
+        __builtin_amdgcn_readfirstlane((int)((groups - 1 - g0) / W + 1));   // groups of this wave
     const int gb = k * bb;
     constexpr bool fused = DECODE && FUSED;            // rows handled here (k <= 64)
 
