@@ -260,48 +260,58 @@ def pmc_traffic(workload, phase, groups):
 
 def packet_protection(eng, k, m, bb, data, parity, steps, stream):
     """The step next to the codec: SerializeFec's encode + seal of the
-    G*m FEC packets (qfec_encode_seal_batch: header || NullEncrypter tag || parity), and the
-    receiver's NullDecrypter open of those packets.  Timed with events on the launch stream;
-    reported beside the bench line, never `value`."""
+    G*m FEC packets (qfec_encode_seal_batch: header || NullEncrypter tag || parity), the seal
+    alone (qfec_null_seal_batch over the same headers and parity), and the receiver's
+    NullDecrypter open of those packets.  Each call is timed from its kernels with the
+    library's timing events (qfec_set_timing_events).  Reported beside the bench line,
+    never `value`."""
     import torch
+    from quic_amd import _lib
+    lib = _lib.load()
     G = data.shape[0]
     n, hl = G * m, 16
     stride = (hl + 12 + bb + 3) // 4 * 4
     dev = data.device
     hdr = torch.arange(n * hl, dtype=torch.int32, device=dev).to(torch.uint8).view(n, hl)
     pkt = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    pkt2 = torch.empty_like(pkt)
     pkt_len = torch.empty(n, dtype=torch.int32, device=dev)
+    pkt_len2 = torch.empty_like(pkt_len)
     # the reference's decrypter copies the whole ciphertext to its output first
     plain = torch.empty((n, (bb + 12 + 3) // 4 * 4), dtype=torch.uint8, device=dev)
     plen = torch.empty(n, dtype=torch.int32, device=dev)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    t = {"encode": 0.0, "encode_seal": 0.0, "open": 0.0}
-    for i in range(steps + 1):
-        ev[0].record(stream)
-        eng.encode(k, m, bb, data, parity)
-        ev[1].record(stream)
-        eng.encode_seal(k, m, bb, data, parity, hdr, hl, pkt, pkt_len)
-        ev[2].record(stream)
-        eng.null_open(pkt, pkt_len, hl, plain, plen)
-        ev[3].record(stream)
-        torch.cuda.synchronize(dev)
-        if i:   # the first pass is warmup
-            t["encode"] += ev[0].elapsed_time(ev[1]) / steps
-            t["encode_seal"] += ev[1].elapsed_time(ev[2]) / steps
-            t["open"] += ev[2].elapsed_time(ev[3]) / steps
-    ok = bool((plen == bb).all()) and torch.equal(plain[:, :bb], parity.view(n, bb))
-    seal_ms = max(t["encode_seal"] - t["encode"], 1e-9)
+    ev = DeviceEvents(6)
+    t = {"encode_seal": 0.0, "seal": 0.0, "open": 0.0}
+    try:
+        for i in range(steps + 1):
+            lib.qfec_set_timing_events(ev.ev[0], ev.ev[1])
+            eng.encode_seal(k, m, bb, data, parity, hdr, hl, pkt, pkt_len)
+            lib.qfec_set_timing_events(ev.ev[2], ev.ev[3])
+            eng.null_seal(hdr, hl, parity.view(n, bb), bb, pkt2, pkt_len2)
+            lib.qfec_set_timing_events(ev.ev[4], ev.ev[5])
+            eng.null_open(pkt, pkt_len, hl, plain, plen)
+            lib.qfec_set_timing_events(None, None)
+            torch.cuda.synchronize(dev)
+            if i:   # the first pass is warmup
+                t["encode_seal"] += ev.elapsed_ms(0, 1) / steps
+                t["seal"] += ev.elapsed_ms(2, 3) / steps
+                t["open"] += ev.elapsed_ms(4, 5) / steps
+    finally:
+        lib.qfec_set_timing_events(None, None)
+        ev.close()
+    ok = (bool((plen == bb).all()) and torch.equal(plain[:, :bb], parity.view(n, bb))
+          and torch.equal(pkt, pkt2))
     pkt_bytes = n * (hl + 12 + bb)
     return {"packets": n, "header_bytes": hl, "encrypter": "NullEncrypter (FNV-1a-128 tag)",
-            "encode_ms": round(t["encode"], 5), "encode_seal_ms": round(t["encode_seal"], 5),
-            "seal_ms": round(seal_ms, 5), "open_ms": round(t["open"], 5),
-            "seal_Mpkt_s": round(n / seal_ms / 1e3, 2),
+            "encode_seal_ms": round(t["encode_seal"], 5), "seal_ms": round(t["seal"], 5),
+            "open_ms": round(t["open"], 5),
+            "seal_Mpkt_s": round(n / t["seal"] / 1e3, 2),
             "open_Mpkt_s": round(n / t["open"] / 1e3, 2),
-            "seal_GBps": round(pkt_bytes / seal_ms / 1e6, 1),
+            "seal_GBps": round(pkt_bytes / t["seal"] / 1e6, 1),
             "open_GBps": round(pkt_bytes / t["open"] / 1e6, 1),
             "round_trip_ok": ok,
-            "note": "seal_ms = encode_seal - encode (same stream, events); one lane per packet "
-                    "(serial FNV chain), DESIGN.md 6.2"}
+            "note": "kernel-bracketing events per call; one lane per packet (serial FNV "
+                    "chain), DESIGN.md 6.2"}
 
 
 def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps, recovered):
