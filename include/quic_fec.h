@@ -148,7 +148,8 @@ QFEC_API int qfec_decode_batch_recovered_host(qfec_ctx *ctx, int k, int m, int b
  * Batches of n packets, all device pointers.  Per-packet lengths come from the int32 arrays,
  * or, where an array is NULL, from the `_all` scalar.  d_out and out_stride must be 4-byte
  * aligned.  d_out_len[i] = bytes written for packet i, or -1 where the reference returns
- * false.
+ * false.  A length larger than its row's stride is rejected (-1, nothing written); a stride
+ * of 0 (every packet reads the same row) is not checked.
  * ------------------------------------------------------------------------------- */
 /* NullEncrypter::EncryptPacket in the EncryptInPlace layout: packet i is
  * AD_i || tag12 || PT_i at d_out + i*out_stride (AD_i at d_ad + i*ad_stride, PT_i at

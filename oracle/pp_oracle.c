@@ -99,7 +99,8 @@ void oracle_null_seal_batch(long long n, const uint8_t *ad, long long ad_stride,
     for (long long i = 0; i < n; ++i) {
         uint8_t *o = out + i * out_stride;
         const long long al = ad_len[i];
-        if (al < 0 || in_len[i] < 0 || out_stride < al + 12 + in_len[i]) {
+        if (al < 0 || in_len[i] < 0 || out_stride < al + 12 + in_len[i] ||
+            (ad_stride && al > ad_stride) || (in_stride && in_len[i] > in_stride)) {
             res[i] = -1; /* nothing written */
             continue;
         }
@@ -117,7 +118,8 @@ void oracle_null_open_batch(long long n, const uint8_t *in, long long in_stride,
     for (long long i = 0; i < n; ++i) {
         const uint8_t *p = in + i * in_stride;
         const long long al = ad_len[i];
-        if (al < 0 || al > in_len[i] || out_stride < in_len[i] - al) {
+        if (al < 0 || al > in_len[i] || out_stride < in_len[i] - al ||
+            (in_stride && in_len[i] > in_stride)) {
             res[i] = -1;
             continue;
         }

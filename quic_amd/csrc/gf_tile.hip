@@ -117,8 +117,12 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
 
     // ---- DMA side: block b of the stream = block iss_x of group G0 + iss_i * GS, into
     // ring buffer iss_slot = b mod NBUF
+    // The stream is extended past its end by re-reads of its last block (at most D of them),
+    // so every block step issues, waits and reads the same way: no tail tests per block, and
+    // the counted waits stay exact up to the last real block.
     int iss_slot = 0;
     int iss_x = 0;
+    int iss_left = nblocks;                          // real blocks not issued yet
     const uint8_t* iss_src = in + G0 * (long long)k * BB;
     const long long gstride = GS * (long long)k * BB;
     auto issue_next = [&]() {
@@ -132,7 +136,7 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
                                              2);
         }
         if (++iss_slot == NBUF) iss_slot = 0;
-        if (++iss_x == k) {
+        if (--iss_left > 0 && ++iss_x == k) {        // after the last block: stay on it
             iss_x = 0;
             iss_src += gstride;
         }
@@ -153,21 +157,17 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
         }
     };
     // wait for block bw's pieces (this wave's), then for every wave's
-    auto wait_block = [&](int bw, bool after_stores) {
-        if (bw + AHEAD < nblocks) {
-            if (after_stores) tile_wait_vmcnt<WAITG>();
-            else tile_wait_vmcnt<WAITN>();
-        } else {
-            tile_wait_vmcnt<0>();   // stream tail: fewer younger pieces
-        }
+    auto wait_block = [&](bool after_stores) {
+        if (after_stores) tile_wait_vmcnt<WAITG>();
+        else tile_wait_vmcnt<WAITN>();
         tile_barrier();
     };
 
+    static_assert(KC >= D, "a group covers the prefetch depth");
 #pragma unroll 1
-    for (int u = 0; u < D; ++u)
-        if (u < nblocks) issue_next();
+    for (int u = 0; u < D; ++u) issue_next();
     uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
-    wait_block(0, false);
+    wait_block(false);
     read_block(0, lo0, hi0);
 
     int b = 0;   // stream index of the current block
@@ -186,13 +186,12 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
         auto step = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
                         uint32_t (&nhi)[8]) __attribute__((always_inline)) {
             constexpr int x = decltype(xc)::value;
-            if (b + D < nblocks) issue_next();
+            issue_next();
             // blocks 0 .. D - 1 of a group were DMA'd before the previous group's stores
-            // were issued, so those stores are younger than their pieces
-            if (b + 1 < nblocks) {
-                wait_block(b + 1, i > 0 && x + 1 <= D - 1);
-                read_block(b + 1, nlo, nhi);
-            }
+            // were issued, so those stores are younger than their pieces (past the stream's
+            // last block this reads a re-read copy nobody uses)
+            wait_block(i > 0 && x + 1 <= D - 1);
+            read_block(b + 1, nlo, nhi);
             ++b;
             WZ v;
 #pragma unroll
@@ -321,6 +320,7 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
     // ---- DMA side: stream block x of group G0 + i * GS = its slot perm[x]
     int iss_slot = 0;
     int iss_x = 0;
+    int iss_left = nblocks;                          // real blocks not issued yet (see above)
     const uint8_t* iss_src = in + G0 * (long long)KC * BB;
     const uint8_t* iss_tab = tab + G0 * tab_gstride;
     const long long gstride = GS * (long long)KC * BB;
@@ -341,7 +341,7 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
                                              2);
         }
         if (++iss_slot == NBUF) iss_slot = 0;
-        if (++iss_x == KC) {
+        if (--iss_left > 0 && ++iss_x == KC) {
             iss_x = 0;
             iss_src += gstride;
             iss_tab += GS * tab_gstride;
@@ -360,21 +360,16 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
             hi[t] = (o & 3) ? q[1] : 0u;
         }
     };
-    auto wait_block = [&](int bw, bool after_stores) __attribute__((always_inline)) {
-        if (bw + AHEAD < nblocks) {
-            if (after_stores) tile_wait_vmcnt<WAITG>();
-            else tile_wait_vmcnt<WAITN>();
-        } else {
-            tile_wait_vmcnt<0>();
-        }
+    auto wait_block = [&](bool after_stores) __attribute__((always_inline)) {
+        if (after_stores) tile_wait_vmcnt<WAITG>();
+        else tile_wait_vmcnt<WAITN>();
         tile_barrier();
     };
 
 #pragma unroll 1
-    for (int u = 0; u < D; ++u)
-        if (u < nblocks) issue_next();
+    for (int u = 0; u < D; ++u) issue_next();
     uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
-    wait_block(0, false);
+    wait_block(false);
     read_block(0, lo0, hi0);
 
     int b = 0;
@@ -399,14 +394,12 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
         // realigned words of block b
         auto advance = [&](const uint32_t (&lo)[8], const uint32_t (&hi)[8], uint32_t (&nlo)[8],
                            uint32_t (&nhi)[8], uint32_t (&wv)[8]) __attribute__((always_inline)) {
-            if (b + D < nblocks) issue_next();
-            if (b + 1 < nblocks) {
-                // positions 0 .. D - 1 of a group were DMA'd before the previous group's
-                // stores were issued, so those stores are younger than their pieces
-                const int p1 = b + 1 - i * KC;
-                wait_block(b + 1, i > 0 && p1 <= D - 1);
-                read_block(b + 1, nlo, nhi);
-            }
+            issue_next();
+            // positions 0 .. D - 1 of a group were DMA'd before the previous group's stores
+            // were issued, so those stores are younger than their pieces
+            const int p1 = b + 1 - i * KC;
+            wait_block(i > 0 && p1 <= D - 1);
+            read_block(b + 1, nlo, nhi);
             ++b;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {

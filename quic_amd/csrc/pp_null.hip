@@ -132,7 +132,10 @@ __global__ __launch_bounds__(kPPWaves * 64) void null_seal_kernel(
     if (mine) {
         al = len_of(ad_len, ad_all, i);
         pl = len_of(pt_len, pt_all, i);
-        ok = al >= 0 && pl >= 0 && (long long)al + 12 + pl <= out_stride;
+        // a row longer than its stride would read the next packet's bytes (or past the
+        // buffer for the last one): rejected like a packet that does not fit
+        ok = al >= 0 && pl >= 0 && (ad_stride == 0 || al <= ad_stride) &&
+             (pt_stride == 0 || pl <= pt_stride) && (long long)al + 12 + pl <= out_stride;
         uint64_t lo, hi;
         fnv_init(lo, hi);
         if (ok) {
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(kPPWaves * 64) void null_open_kernel(
         al = len_of(ad_len, ad_all, i);
         const int tl = len_of(pkt_len, pkt_all, i);
         cl = tl - al;   // ciphertext bytes
-        copy = al >= 0 && cl >= 0 && cl <= out_stride;
+        copy = al >= 0 && cl >= 0 && cl <= out_stride && (pkt_stride == 0 || tl <= pkt_stride);
         if (copy && cl >= 12) {
             const uint8_t* c = p + al;
             uint32_t t[3];

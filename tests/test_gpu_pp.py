@@ -143,3 +143,32 @@ def test_full_size_round_trip(engine):
     engine.null_open(bad, pkt_len, 16, plain, plen)
     torch.cuda.synchronize()
     assert bool((plen == -1).all())
+
+
+def test_lengths_beyond_row_stride_rejected(engine, oracle):
+    # a length larger than its row's stride would read the next row (past the buffer for
+    # the last one): rejected with -1 and nothing written, in the oracle and on the GPU
+    import torch
+    rng = np.random.default_rng(9)
+    n, AS, S = 6, 16, 64
+    ad = rng.integers(0, 256, (n, AS), dtype=np.uint8)
+    pt = rng.integers(0, 256, (n, S), dtype=np.uint8)
+    ad_len = np.array([16, 17, 0, 16, 3, 16], np.int32)
+    pt_len = np.array([64, 10, 65, 0, 64, 1000], np.int32)
+    exp, eres = oracle.null_seal_batch(ad, ad_len, pt, pt_len, 2048)
+    assert list(eres < 0) == [False, True, True, False, False, True]
+    out = torch.zeros((n, 2048), dtype=torch.uint8, device="cuda")
+    out_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.null_seal(_dev(ad), _dev(ad_len), _dev(pt), _dev(pt_len), out, out_len)
+    assert np.array_equal(_host(out_len), eres)
+    assert np.array_equal(_host(out), exp)
+    pkt = exp[:, :128].copy()
+    pkt_len = np.array([92, 129, 40, 28, 200, 12], np.int32)   # 129, 200 > stride 128
+    adl = np.array([16, 16, 0, 16, 3, 12], np.int32)
+    exp_o, eres_o = oracle.null_open_batch(pkt, pkt_len, adl, 256)
+    assert eres_o[1] == -1 and eres_o[4] == -1 and not exp_o[1].any() and not exp_o[4].any()
+    out_o = torch.zeros((n, 256), dtype=torch.uint8, device="cuda")
+    len_o = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.null_open(_dev(pkt), _dev(pkt_len), _dev(adl), out_o, len_o)
+    assert np.array_equal(_host(len_o), eres_o)
+    assert np.array_equal(_host(out_o), exp_o)

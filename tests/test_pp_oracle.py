@@ -112,3 +112,14 @@ def test_batch_layout_and_edges(oracle):
         else:
             assert ores[i] == pt_len[i]
             assert opened[i, :pt_len[i]].tobytes() == pt[i, :pt_len[i]].tobytes()
+
+
+def test_batch_rejects_lengths_beyond_stride(oracle):
+    ad = np.zeros((2, 8), np.uint8)
+    pt = np.zeros((2, 8), np.uint8)
+    _, res = oracle.null_seal_batch(ad, np.array([9, 8], np.int32), pt,
+                                    np.array([8, 9], np.int32), 64)
+    assert list(res) == [-1, -1]
+    _, res = oracle.null_open_batch(np.zeros((2, 32), np.uint8), np.array([33, 32], np.int32),
+                                    np.array([0, 0], np.int32), 64)
+    assert res[0] == -1 and res[1] == -1   # 33 > stride; 32 bytes: a bad tag
