@@ -86,7 +86,7 @@ QFEC_API void qfec_ctx_destroy(qfec_ctx *ctx);
 /* Launch-shape options of one context (the defaults are the measured best):
  * "xor_slots" 2..4, "xor_waves" 1..4, "dma" 0/1, "stream" 0/1, "stream_ring" 4..36,
  * "stream_grid" 0.., "const_enc" 0/1, "stream_static" 0/1, "tile" 0/1,
- * "tile_grid" 0.., "tile_depth" 4/6, "pd" 1..3, "flat" 0/1, "enc_rc" 2/4/8, "prep_lane" 0/1,
+ * "tile_grid" 0.., "tile_depth" 4/6, "tile_pair" 0/1, "pd" 1..3, "flat" 0/1, "enc_rc" 2/4/8, "prep_lane" 0/1,
  * "host_chunk_mb" 1..4096.  get also reads "cus" (compute units of the device).
  * -2 for an unknown name or a value out of range.  No environment variable changes
  * what the library launches. */

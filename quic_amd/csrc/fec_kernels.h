@@ -29,6 +29,7 @@ struct Tune {
     int tile = 1;             // (128, 16) x 9008 B: gf_tile / gf_tile_syn (0: gf_apply)
     int tile_grid = 0;        // gf_tile: grid cap in workgroups (0: CUs x per-CU fit)
     int tile_depth = 6;       // gf_tile: blocks in flight per workgroup (4 or 6)
+    int tile_pair = 1;        // gf_tile encode: one workgroup barrier per two blocks (depth 6)
     int pd = 2;               // gf_apply: register pipeline depth (1..3)
     int flat = 1;             // gf_apply: lane-flat encode
     int enc_rc = 8;           // gf_apply: encode outputs per wave (2, 4, 8)

@@ -78,8 +78,10 @@ struct TileShape {
 };
 
 // S: sub-row bytes (compile time).  RC: outputs per chunk wave, NCH chunks.  D: blocks in
-// flight (D + 2 LDS buffers).  Encode of the compiled code (k, m) = (KC, MC).
-template <int S, int RC, int NCH, int D, int KC, int MC>
+// flight (D + 1 + BP LDS buffers).  Encode of the compiled code (k, m) = (KC, MC).
+// BP: blocks per workgroup barrier (1, or 2: even steps wait for the next two blocks'
+// pieces and pass one barrier for both; odd steps neither wait nor synchronise).
+template <int S, int RC, int NCH, int D, int KC, int MC, int BP = 1>
 __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
                              (TileShape<S>::NT * NCH + 3) / 4) void gf_tile_kernel(
     const uint8_t* in, uint8_t* out, long long groups, long long out_gstride) {
@@ -88,15 +90,19 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
     constexpr int BBP = T::BBP, SPR = T::SPR;
     constexpr int NWV = NT * NCH;
     constexpr int PPW = (NPB + NWV - 1) / NWV;     // pieces per wave per block
-    // D blocks in flight plus two buffers: the one being read and the one the slowest wave
+    // D blocks in flight plus 1 + BP buffers: the one being read and those the slowest wave
     // may still have LDS reads outstanding on (a wave issues the DMA of block b + D after it
-    // passed the barrier of block b, so every wave has consumed block b - 2 by then)
-    constexpr int NBUF = D + 2;
+    // passed a barrier that every wave reached after consuming block b - 1 - BP)
+    constexpr int NBUF = D + 1 + BP;
     constexpr int NST = RC * 8 * SPR;               // stores per wave per group
     // block b + 1's LDS reads are issued before block b is combined (register double buffer)
     constexpr int AHEAD = D - 1;                     // blocks issued after the awaited one
     constexpr int WAITN = AHEAD * PPW;
     constexpr int WAITG = AHEAD * PPW + NST > 63 ? 63 : AHEAD * PPW + NST;
+    // pair barriers: an even step waits for block b + 2, with D - 2 blocks issued after it
+    constexpr int WAITN2 = (D - 2) * PPW;
+    constexpr int WAITG2 = (D - 2) * PPW + NST > 63 ? 63 : (D - 2) * PPW + NST;
+    static_assert(BP == 1 || (BP == 2 && D >= 3 && KC % 2 == 0), "pair barriers");
     constexpr int SAUX = 2;                          // the dense parity stream: nt stores
     static_assert(S % 2 == 0 && BB % 16 == 0, "16-byte aligned blocks, 2-byte aligned sub-rows");
     static_assert(MC > 0 && (MC + RC - 1) / RC == NCH && KC % 2 == 0, "compiled code");
@@ -190,7 +196,16 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
             // blocks 0 .. D - 1 of a group were DMA'd before the previous group's stores
             // were issued, so those stores are younger than their pieces (past the stream's
             // last block this reads a re-read copy nobody uses)
-            wait_block(i > 0 && x + 1 <= D - 1);
+            if constexpr (BP == 1) {
+                wait_block(i > 0 && x + 1 <= D - 1);
+            } else if constexpr (x % 2 == 0) {
+                // blocks b + 1 and b + 2 (in order: waiting for b + 2 covers b + 1); block
+                // x + 2 of this group, or block 0 of the next (whose preceding stores are
+                // not issued yet)
+                if (i > 0 && x + 2 <= D - 1) tile_wait_vmcnt<WAITG2>();
+                else tile_wait_vmcnt<WAITN2>();
+                tile_barrier();
+            }
             read_block(b + 1, nlo, nhi);
             ++b;
             WZ v;
@@ -636,9 +651,11 @@ hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, 
     if (!gf_tile_supported(k, m, bb, t)) return hipErrorInvalidValue;
     if (((uintptr_t)in & 15) != 0) return hipErrorInvalidValue;
     if (t.tile_depth != 4 && t.tile_depth != 6) return hipErrorInvalidValue;
+    const bool pair = t.tile_pair && t.tile_depth == 6;   // depth 4: one barrier per block
     using TS = TileShape<kTileS>;
     constexpr int nch = 2;
-    const size_t lds = (size_t)(t.tile_depth + 2) * TS::BBP;
+    const int bp = pair ? 2 : 1;
+    const size_t lds = (size_t)(t.tile_depth + 1 + bp) * TS::BBP;
     const unsigned threads = (unsigned)(TS::NT * nch * 64);
     // workgroups per CU: LDS and 16 waves (<= 128 VGPRs: 4 waves per SIMD)
     const int per_cu = std::max(1, std::min((int)((160 * 1024) / lds), 16 / (TS::NT * nch)));
@@ -647,7 +664,10 @@ hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, 
     const unsigned grid = (unsigned)std::min<long long>(groups, cap);
     if ((groups + grid - 1) / grid * k >= (1LL << 31)) return hipErrorInvalidValue;
     note_kernel("gf_tile_kernel<encode,k128m16>");
-    if (t.tile_depth == 4)
+    if (pair)
+        qlaunch((gf_tile_kernel<kTileS, 8, nch, 6, 128, 16, 2>), dim3(grid), dim3(threads),
+                lds, st, in, out, groups, out_gstride);
+    else if (t.tile_depth == 4)
         qlaunch((gf_tile_kernel<kTileS, 8, nch, 4, 128, 16>), dim3(grid), dim3(threads),
                            lds, st, in, out, groups, out_gstride);
     else

@@ -394,7 +394,7 @@ OPTION_SETS = [
     {"dma": 0}, {"stream": 0}, {"stream": 0, "pd": 1}, {"stream": 0, "pd": 3},
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
     {"stream_ring": 36}, {"host_chunk_mb": 1}, {"const_enc": 0}, {"tile": 0},
-    {"tile_depth": 4}, {"stream_static": 0},
+    {"tile_depth": 4}, {"tile_pair": 0}, {"stream_static": 0},
 ]
 
 
@@ -612,7 +612,7 @@ def test_stream_any_small_block(engine, oracle, bb, k, m, r):
 
 
 # ------------------------------------------------- gf_tile (9008-byte blocks, config D)
-@pytest.mark.parametrize("depth", [4, 6])
+@pytest.mark.parametrize("depth", [4, 6, "6p"])
 @pytest.mark.parametrize("grid", [1, 3, 0])
 @pytest.mark.parametrize("k,m,r", [(128, 16, 8), (128, 16, 13), (40, 16, 16), (16, 6, 4)])
 def test_tile_many_groups_per_workgroup(tuned_engine, oracle, depth, grid, k, m, r):
@@ -621,7 +621,8 @@ def test_tile_many_groups_per_workgroup(tuned_engine, oracle, depth, grid, k, m,
     in the vmcnt count); every third group has no loss."""
     engine = tuned_engine
     engine.set_option("tile_grid", grid)
-    engine.set_option("tile_depth", depth)
+    engine.set_option("tile_depth", 6 if depth == "6p" else depth)
+    engine.set_option("tile_pair", 1 if depth == "6p" else 0)   # one barrier per 2 blocks
     bb, G = 9008, 7
     data = synth.group_data(4000 + k + m + grid, k, bb, G)
     p_or, rc_or = oracle.encode_batch(k, m, bb, data)
