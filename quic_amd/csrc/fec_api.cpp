@@ -229,7 +229,9 @@ int get_cenc(qfec_ctx* c, int k, int m, const uint8_t** out) {
 int decode_workspace(qfec_ctx* c, int k, int rmax, int rc, long long groups) {
     const int rcp = std::max(rc, 4);
     const int nchunk = (rmax + rc - 1) / rc;
-    QF_HIP(c->dcoef.ensure((size_t)groups * nchunk * k * rcp));
+    // per group: the apply coefficients, or a syndrome table (bsyn:: / syn::)
+    const size_t per = std::max<size_t>((size_t)nchunk * k * rcp, qfec::bsyn::kBytes);
+    QF_HIP(c->dcoef.ensure((size_t)groups * per));
     QF_HIP(c->dslots.ensure((size_t)groups * rmax));
     QF_HIP(c->dnout.ensure((size_t)groups * sizeof(int32_t)));
     return 0;
@@ -309,6 +311,15 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
                                              c->tune));
         return 0;
     }
+    if (qfec::gf_bsyn_supported(k, m, bb, rmax, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
+        // compiled (32, 4) code: syndromes of every parity row, then the r x r solve (a
+        // group's stores follow all of its reads: in place needs no scratch)
+        QF_HIP(qfec::launch_decode_prep_bsyn(d_rows_in, d_rows_out, d_status, cenc, w.coef,
+                                             w.slots, w.nout, nullptr, k, m, bb, rmax, G, st));
+        QF_HIP(qfec::launch_gf_bsyn(d_blocks, d_out, w.coef, cenc, w.slots, w.nout, k, m, bb, G,
+                                    rmax, (long long)k * bb, st, c->tune));
+        return 0;
+    }
     QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc, rmax,
                                     G, st, c->tune));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
@@ -380,6 +391,13 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
         QF_HIP(qfec::launch_gf_tile_syndrome(d_blocks, d_rec, w.coef, nullptr, w.nout, cenc, k, m,
                                              bb, G, rmax, (long long)nchunk * k * std::max(rc, 4),
                                              (long long)rmax * bb, st, c->tune));
+        return 0;
+    }
+    if (qfec::gf_bsyn_supported(k, m, bb, rmax, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
+        QF_HIP(qfec::launch_decode_prep_bsyn(d_rows_in, nullptr, d_status, cenc, w.coef, w.slots,
+                                             w.nout, d_rec_rows, k, m, bb, rmax, G, st));
+        QF_HIP(qfec::launch_gf_bsyn(d_blocks, d_rec, w.coef, cenc, nullptr, w.nout, k, m, bb, G,
+                                    rmax, (long long)rmax * bb, st, c->tune));
         return 0;
     }
     QF_HIP(qfec::launch_decode_prep(d_rows_in, nullptr, d_status, cenc, w, k, m, bb, rc, rmax, G,
@@ -534,6 +552,8 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"const_enc", &t.const_enc, 0, 1},     {"tile", &t.tile, 0, 1},
         {"stream_static", &t.stream_static, 0, 1},
         {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_depth", &t.tile_depth, 4, 6}, {"tile_pair", &t.tile_pair, 0, 1},
+        {"tile_occ2", &t.tile_occ2, 0, 1},
+        {"bsyn", &t.bsyn, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -541,7 +561,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
     for (const Opt& o : opts) {
         if (strcmp(o.n, name) != 0) continue;
         if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))) ||
-            (o.p == &t.tile_depth && value != 4 && value != 6))
+            (o.p == &t.tile_depth && value == 5 && !t.tile_occ2))
             return fail(-2, std::string("option value out of range: ") + name);
         *o.p = value;
         return 0;
@@ -557,7 +577,8 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
         {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"tile", t.tile}, {"tile_grid", t.tile_grid},
-        {"tile_depth", t.tile_depth}, {"tile_pair", t.tile_pair},
+        {"tile_depth", t.tile_depth}, {"tile_pair", t.tile_pair}, {"tile_occ2", t.tile_occ2},
+        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb},
     };
@@ -819,6 +840,7 @@ int qfec_decode_batch_host(qfec_ctx* c, int k, int m, int bb, long long groups,
 
 int qfec_synth_fill(void* d_dst, unsigned long long bytes, unsigned long long seed,
                     unsigned long long byte_offset, void* stream) {
+    qfec::TimingMute mute;
     QF_HIP(qfec::launch_synth_fill((uint8_t*)d_dst, bytes, seed, byte_offset,
                                    (hipStream_t)stream));
     return 0;
@@ -827,6 +849,7 @@ int qfec_synth_fill(void* d_dst, unsigned long long bytes, unsigned long long se
 int qfec_synth_gather(const unsigned char* d_data, const unsigned char* d_parity,
                       const short* d_src, unsigned char* d_blocks, int k, int m, int bb,
                       long long groups, void* stream) {
+    qfec::TimingMute mute;
     QF_HIP(qfec::launch_synth_gather(d_data, d_parity, (const int16_t*)d_src, d_blocks, k, m, bb,
                                      groups, (hipStream_t)stream));
     return 0;

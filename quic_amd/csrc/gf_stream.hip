@@ -620,6 +620,21 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
     stream_wait_vmcnt<0>();
 }
 
+// Ring slots the stream needs: before block x's compute the ring keeps every piece from
+// block x's first on, and block x + 1 must land in it too.  Blocks x and x + 1 span
+// (o + 2 * bb + 1023) / 1024 pieces from block x's head piece, o its start offset in that
+// piece; o is a multiple of gcd(bb, 1024), so at most 1024 - gcd(bb, 1024).
+int gf_stream_min_ring(int bb) {
+    int a = bb, b = 1024;
+    while (b) {
+        const int r = a % b;
+        a = b;
+        b = r;
+    }
+    const int max_o = 1024 - a;
+    return (max_o + 2 * bb + 1023) / 1024;
+}
+
 bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& t) {
     (void)m;
     (void)decode;
@@ -627,6 +642,7 @@ bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& 
     if (bb % 8 != 0 || bb < 8 || bb > 2048) return false;   // s <= 256: a word per lane
     if (rc != 2 && rc != 4 && rc != 8) return false;
     if (((long long)k * bb) % 16 != 0 || (long long)k * bb < 16) return false;
+    if (t.stream_ring < gf_stream_min_ring(bb)) return false;   // gf_apply instead
     return true;
 }
 
@@ -649,6 +665,12 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     const unsigned grid = (unsigned)std::min<long long>(want, cap);
     const unsigned threads = kStreamWaves * 64;
     const int s = bb / 8;
+    // the wave's 32-bit piece counters: cnt * NP, and (gf_ring) cnt groups
+    {
+        const long long waves = (long long)grid * kStreamWaves;
+        const long long np = ((long long)k * bb + 1023) / 1024;
+        if ((groups + waves - 1) / waves * np >= (1LL << 31)) return hipErrorInvalidValue;
+    }
 #define QS_GO(RCV, SV, DEC, RCPV, KCV)                                                        \
     qlaunch((gf_stream_kernel<RCV, SV, DEC, RCPV, KCV>), dim3(grid), dim3(threads), \
                        lds, st, in, out, coef, slots, nout, groups, k, m, rmax, coef_gstride,   \
@@ -681,6 +703,9 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         long long rcap = (long long)t.cus * (int)((160 * 1024) / rlds);
         if (t.stream_grid > 0) rcap = t.stream_grid;
         const unsigned rgrid = (unsigned)std::min<long long>(rwant, rcap);
+        if ((groups + (long long)rgrid * kRingWaves - 1) / ((long long)rgrid * kRingWaves) >=
+            (1LL << 31))
+            return hipErrorInvalidValue;
 #define QR_GO(RCV, DEC, MCV)                                                                   \
     qlaunch((gf_ring_kernel<32, 169, RCV, DEC, MCV>), dim3(rgrid),                   \
                        dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax, \

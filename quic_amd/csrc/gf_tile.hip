@@ -66,6 +66,40 @@ __device__ __forceinline__ uint32_t tile_cload_u32(const uint8_t* base, int byte
 
 constexpr unsigned kTDrop = 0x80000000u;   // buffer offset past any range: lane dropped
 
+// The lane id recomputed where it is used (v_mbcnt), in a volatile asm the compiler may not
+// hoist: values derived from it at a group's end are not kept live (or spilled) across the
+// block loop.
+// (The host pass parses these bodies too, and an AMDGPU register constraint there would void
+// the kernel's host stub; the asm is emitted for the device only.)
+__device__ __forceinline__ int tile_lane_here() {
+    int l = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+#endif
+    return l;
+}
+
+// 16 bytes per lane from buffer rs at voff + soff into LDS at lds + 16 * lane (nt), i.e.
+// buffer_load_dwordx4 ... lds: one VGPR of address (device only, as above: in a lambda the
+// builtin voids the host stub)
+__device__ __forceinline__ void tile_dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds,
+                                           uint32_t voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, QT_LPTR(lds), 16, voff, soff, 0, 2);
+#else
+    (void)rs, (void)lds, (void)voff, (void)soff;
+#endif
+}
+
+// an SGPR value made opaque to the optimiser (device only, as above)
+__device__ __forceinline__ void tile_opaque_s(int& x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(x));
+#else
+    (void)x;
+#endif
+}
+
 template <int S>
 struct TileShape {
     static constexpr int BB = 8 * S;
@@ -81,9 +115,12 @@ struct TileShape {
 // flight (D + 1 + BP LDS buffers).  Encode of the compiled code (k, m) = (KC, MC).
 // BP: blocks per workgroup barrier (1, or 2: even steps wait for the next two blocks'
 // pieces and pass one barrier for both; odd steps neither wait nor synchronise).
-template <int S, int RC, int NCH, int D, int KC, int MC, int BP = 1>
-__global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
-                             (TileShape<S>::NT * NCH + 3) / 4) void gf_tile_kernel(
+// DB: block b + 1's LDS reads are issued before block b is combined (register double
+// buffer, 111 VGPRs: one 10-wave workgroup per CU).  !DB: a block is read right before it
+// is combined and the kernel is held to 96 VGPRs, so two workgroups share a CU (5 waves per
+// SIMD, the SIMDs evenly loaded; the other workgroup's waves hide the LDS latency).
+template <int S, int RC, int NCH, int D, int KC, int MC, int BP = 1, bool DB = true>
+__global__ __launch_bounds__(TileShape<S>::NT * NCH * 64, DB ? 3 : 5) void gf_tile_kernel(
     const uint8_t* in, uint8_t* out, long long groups, long long out_gstride) {
     using T = TileShape<S>;
     constexpr int BB = T::BB, NW = T::NW, NWF = T::NWF, NT = T::NT, NPB = T::NPB;
@@ -102,6 +139,12 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
     // pair barriers: an even step waits for block b + 2, with D - 2 blocks issued after it
     constexpr int WAITN2 = (D - 2) * PPW;
     constexpr int WAITG2 = (D - 2) * PPW + NST > 63 ? 63 : (D - 2) * PPW + NST;
+    // !DB: the step waits for its own block (D issued after it), pairs for b + 1 (D - 1)
+    constexpr int WAITNS = D * PPW;
+    constexpr int WAITGS = D * PPW + NST > 63 ? 63 : D * PPW + NST;
+    constexpr int WAITN2S = (D - 1) * PPW;
+    constexpr int WAITG2S = (D - 1) * PPW + NST > 63 ? 63 : (D - 1) * PPW + NST;
+    static_assert(DB || WAITNS <= 63, "pipeline depth");
     static_assert(BP == 1 || (BP == 2 && D >= 3 && KC % 2 == 0), "pair barriers");
     constexpr int SAUX = 2;                          // the dense parity stream: nt stores
     static_assert(S % 2 == 0 && BB % 16 == 0, "16-byte aligned blocks, 2-byte aligned sub-rows");
@@ -111,7 +154,9 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
 
     const int lane = threadIdx.x & 63;
     const int w = wave_id();
-    const int tile = w % NT, chunk = w / NT;
+    // wave-uniform (SGPRs: a VGPR copy of the chunk would be one more live register)
+    const int tile = __builtin_amdgcn_readfirstlane(w % NT);
+    const int chunk = __builtin_amdgcn_readfirstlane(w / NT);
     const int c = min(tile * 64 + lane, NW - 1);     // idle lanes shadow the last word
     constexpr int k = KC;
     const long long G0 = blockIdx.x, GS = gridDim.x;
@@ -131,15 +176,22 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
     int iss_left = nblocks;                          // real blocks not issued yet
     const uint8_t* iss_src = in + G0 * (long long)k * BB;
     const long long gstride = GS * (long long)k * BB;
+    // buffer_load ... lds: the group's base in a buffer resource (SGPRs), the block offset in
+    // soffset, the lane's piece offset (fixed per wave) in one VGPR
+    uint32_t voff[PPW];
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+        const int p = min(w + q * NWV, NPB - 1);   // surplus waves reload the last piece
+        voff[q] = (uint32_t)min(p * 1024 + lane * 16, BB - 16);
+    }
     auto issue_next = [&]() {
         uint8_t* dst = smem + iss_slot * BBP;
-        const uint8_t* src = iss_src + (long long)iss_x * BB;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)iss_src, 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
         for (int q = 0; q < PPW; ++q) {
-            const int p = min(w + q * NWV, NPB - 1);   // surplus waves reload the last piece
-            const int off = min(p * 1024 + lane * 16, BB - 16);
-            __builtin_amdgcn_global_load_lds(QT_GPTR(src + off), QT_LPTR(dst + p * 1024), 16, 0,
-                                             2);
+            const int p = min(w + q * NWV, NPB - 1);
+            tile_dma16(rs, dst + p * 1024, voff[q], iss_x * BB);
         }
         if (++iss_slot == NBUF) iss_slot = 0;
         if (--iss_left > 0 && ++iss_x == k) {        // after the last block: stay on it
@@ -173,8 +225,10 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
 #pragma unroll 1
     for (int u = 0; u < D; ++u) issue_next();
     uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
-    wait_block(false);
-    read_block(0, lo0, hi0);
+    if constexpr (DB) {
+        wait_block(false);
+        read_block(0, lo0, hi0);
+    }
 
     int b = 0;   // stream index of the current block
 #pragma unroll 1
@@ -196,7 +250,20 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
             // blocks 0 .. D - 1 of a group were DMA'd before the previous group's stores
             // were issued, so those stores are younger than their pieces (past the stream's
             // last block this reads a re-read copy nobody uses)
-            if constexpr (BP == 1) {
+            if constexpr (!DB) {
+                // block b itself: D blocks issued after it; pair barriers wait at even steps
+                // for blocks b and b + 1 (D - 1 after it; both of this group: KC is even)
+                if constexpr (BP == 1) {
+                    if (i > 0 && x <= D - 1) tile_wait_vmcnt<WAITGS>();
+                    else tile_wait_vmcnt<WAITNS>();
+                    tile_barrier();
+                } else if constexpr (x % 2 == 0) {
+                    if (i > 0 && x + 1 <= D - 1) tile_wait_vmcnt<WAITG2S>();
+                    else tile_wait_vmcnt<WAITN2S>();
+                    tile_barrier();
+                }
+                read_block(b, lo, hi);
+            } else if constexpr (BP == 1) {
                 wait_block(i > 0 && x + 1 <= D - 1);
             } else if constexpr (x % 2 == 0) {
                 // blocks b + 1 and b + 2 (in order: waiting for b + 2 covers b + 1); block
@@ -206,7 +273,7 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
                 else tile_wait_vmcnt<WAITN2>();
                 tile_barrier();
             }
-            read_block(b + 1, nlo, nhi);
+            if constexpr (DB) read_block(b + 1, nlo, nhi);
             ++b;
             WZ v;
 #pragma unroll
@@ -220,9 +287,13 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
             // chunk, behind a uniform branch.
             Win win;
             win_build(v.W8, win);
+            // the chunk test on an SGPR value per block (a loop-invariant condition is kept
+            // as a lane mask across the block loop, i.e. in a VGPR)
+            int chv = chunk;
+            tile_opaque_s(chv);
             static_for<NCH>([&](auto chc) __attribute__((always_inline)) {
                 constexpr int CH = decltype(chc)::value;
-                if (chunk == CH) {
+                if (chv == CH) {
                     static_for<RC>([&](auto jc) __attribute__((always_inline)) {
                         constexpr int o = CH * RC + decltype(jc)::value;
                         if constexpr (o < MC)
@@ -241,12 +312,12 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
                 for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
             // and no instruction scheduled across blocks (register pressure)
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (decltype(xc)::value % 2 == 0)
+            if constexpr (!DB || decltype(xc)::value % 2 == 0)
                 step(xc, lo0, hi0, lo1, hi1);
             else
                 step(xc, lo1, hi1, lo0, hi0);
         });
-        // KC is even: the next group's first block is in lo0/hi0 again
+        // KC is even: the next group's first block is in lo0/hi0 again (DB)
 
         // ---- outputs: a fixed number of store instructions (unused outputs, idle lanes
         // and the lanes outside a word's valid bytes are dropped)
@@ -255,7 +326,8 @@ __global__ __launch_bounds__(TileShape<S>::NT * NCH * 64,
         // so the whole phase needs two VGPRs of addresses (opaque: not hoisted out of the
         // group loop as 8 x RC precomputed offsets).
         asm volatile("" ::: "memory");   // stores stay in issue order among the DMAs
-        const bool live = tile * 64 + lane < NW;
+        const int lane_e = tile_lane_here();
+        const bool live = tile * 64 + lane_e < NW;
         uint32_t vo = live && c < NWF ? 4u * (uint32_t)c : kTDrop;
         uint32_t vt = live && c == NWF && NWF < NW ? 4u * (uint32_t)c : kTDrop;
         asm volatile("" : "+v"(vo), "+v"(vt));
@@ -325,7 +397,9 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
 
     const int lane = threadIdx.x & 63;
     const int w = wave_id();
-    const int tile = w % NT, chunk = w / NT;
+    // wave-uniform (SGPRs: a VGPR copy of the chunk would be one more live register)
+    const int tile = __builtin_amdgcn_readfirstlane(w % NT);
+    const int chunk = __builtin_amdgcn_readfirstlane(w / NT);
     const int c = min(tile * 64 + lane, NW - 1);
     const long long G0 = blockIdx.x, GS = gridDim.x;
     if (G0 >= groups) return;
@@ -527,7 +601,8 @@ gf_tile_syn_kernel(const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ 
         // path issues the same store count (outputs past n with an empty range).
         uint32_t* tlw = tl + tile * 8 * 64 + lane;   // + (i * NT * 8 + r) * 64
         asm volatile("" ::: "memory");   // stores stay in issue order among the DMAs
-        const bool live = tile * 64 + lane < NW;
+        const int lane_e = tile_lane_here();
+        const bool live = tile * 64 + lane_e < NW;
         uint32_t vo = live && c < NWF ? 4u * (uint32_t)c : kTDrop;
         uint32_t vt = live && c == NWF && NWF < NW ? 4u * (uint32_t)c : kTDrop;
         asm volatile("" : "+v"(vo), "+v"(vt));
@@ -650,20 +725,39 @@ hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, 
     if (groups <= 0) return hipSuccess;
     if (!gf_tile_supported(k, m, bb, t)) return hipErrorInvalidValue;
     if (((uintptr_t)in & 15) != 0) return hipErrorInvalidValue;
-    if (t.tile_depth != 4 && t.tile_depth != 6) return hipErrorInvalidValue;
-    const bool pair = t.tile_pair && t.tile_depth == 6;   // depth 4: one barrier per block
+    if (t.tile_depth != 4 && t.tile_depth != 6 && !(t.tile_occ2 && t.tile_depth == 5))
+        return hipErrorInvalidValue;
+    const bool pair = t.tile_pair && t.tile_depth >= 5;   // depth 4: one barrier per block
     using TS = TileShape<kTileS>;
     constexpr int nch = 2;
     const int bp = pair ? 2 : 1;
     const size_t lds = (size_t)(t.tile_depth + 1 + bp) * TS::BBP;
     const unsigned threads = (unsigned)(TS::NT * nch * 64);
-    // workgroups per CU: LDS and 16 waves (<= 128 VGPRs: 4 waves per SIMD)
-    const int per_cu = std::max(1, std::min((int)((160 * 1024) / lds), 16 / (TS::NT * nch)));
+    // workgroups per CU: LDS and waves (<= 128 VGPRs: 16 waves; occ2: <= 96 VGPRs, 20 waves)
+    const int wave_cap = t.tile_occ2 ? 20 : 16;
+    const int per_cu = std::max(1, std::min((int)((160 * 1024) / lds), wave_cap / (TS::NT * nch)));
     long long cap = (long long)t.cus * per_cu;
     if (t.tile_grid > 0) cap = t.tile_grid;              // tests: many groups per workgroup
     const unsigned grid = (unsigned)std::min<long long>(groups, cap);
     if ((groups + grid - 1) / grid * k >= (1LL << 31)) return hipErrorInvalidValue;
-    note_kernel("gf_tile_kernel<encode,k128m16>");
+    note_kernel(t.tile_occ2 ? "gf_tile_kernel<encode,k128m16,occ2>" : "gf_tile_kernel<encode,k128m16>");
+    if (t.tile_occ2) {
+        // two workgroups per CU: LDS <= 80 KB each, the register double buffer dropped
+        if (lds > 80 * 1024) return hipErrorInvalidValue;
+        if (pair && t.tile_depth == 5)
+            qlaunch((gf_tile_kernel<kTileS, 8, nch, 5, 128, 16, 2, false>), dim3(grid),
+                    dim3(threads), lds, st, in, out, groups, out_gstride);
+        else if (!pair && t.tile_depth == 6)
+            qlaunch((gf_tile_kernel<kTileS, 8, nch, 6, 128, 16, 1, false>), dim3(grid),
+                    dim3(threads), lds, st, in, out, groups, out_gstride);
+        else if (!pair && t.tile_depth == 4)
+            qlaunch((gf_tile_kernel<kTileS, 8, nch, 4, 128, 16, 1, false>), dim3(grid),
+                    dim3(threads), lds, st, in, out, groups, out_gstride);
+        else
+            return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
+    if (t.tile_depth == 5) return hipErrorInvalidValue;
     if (pair)
         qlaunch((gf_tile_kernel<kTileS, 8, nch, 6, 128, 16, 2>), dim3(grid), dim3(threads),
                 lds, st, in, out, groups, out_gstride);

@@ -207,6 +207,9 @@ hipError_t xor_go(const XorPlan& p, const uint8_t* in, uint8_t* out, const uint8
                                                                 status, k, bb, G, ogs, st, cus);
         const long long want = (G + p.waves - 1) / p.waves;
         const unsigned nb = (unsigned)std::min<long long>(want, (long long)cus);
+        // the wave's group count is a 32-bit SGPR value
+        if ((G + (long long)nb * p.waves - 1) / ((long long)nb * p.waves) >= (1LL << 31))
+            return hipErrorInvalidValue;
         note_kernel(DECODE ? (COMPACT ? "xor_dma_kernel<decode,recovered>"
                                       : "xor_dma_kernel<decode>")
                            : "xor_dma_kernel<encode>");

@@ -36,6 +36,16 @@ def test_library_exports_every_header_symbol():
     assert not extra, extra
 
 
+def test_no_undefined_kernel_handles():
+    """Every kernel the launchers name has its host-side handle in the library (a kernel
+    body the host pass cannot compile drops the handle silently, and the library then fails
+    to load on the GPU box)."""
+    out = subprocess.run(["nm", "-u", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    missing = [line.split()[-1] for line in out.splitlines() if "4qfec" in line]
+    assert not missing, missing
+
+
 def test_ctypes_signatures_cover_header():
     from quic_amd import fec_group
     assert header_symbols() <= set(_lib.SIGNATURES) | set(fec_group._SIG)

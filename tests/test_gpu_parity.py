@@ -388,6 +388,34 @@ def test_stream_ring_many_groups_per_wave(tuned_engine, oracle, ring, k, m, r):
     np.testing.assert_array_equal(got[mask], exp[mask])
 
 
+@pytest.mark.parametrize("ring", [4, 5])
+@pytest.mark.parametrize("bb", [2040, 1544, 2048])
+def test_stream_ring_too_small_for_block(tuned_engine, oracle, ring, bb):
+    """A ring must hold blocks x and x + 1 from block x's head piece: up to
+    (1024 - gcd(bb, 1024) + 2 bb + 1023) / 1024 slots (5 for bb = 2040 or 1544, 4 for
+    2048).  With a smaller ring the library does not launch gf_stream (it would read a
+    slot whose piece was never issued); the result stays bit-exact either way."""
+    engine = tuned_engine
+    engine.set_option("stream_grid", 1)
+    engine.set_option("stream_ring", ring)
+    k, m, r, G = 8, 4, 3, 9
+    data = synth.group_data(bb + ring, k, bb, G)
+    p_or, _ = oracle.encode_batch(k, m, bb, data)
+    p_gpu, rc = gpu_encode(engine, k, m, bb, data)
+    streamed = "gf_stream" in fec.last_kernels()
+    assert streamed == (bb == 2048 or ring >= 5)
+    assert rc == 0
+    np.testing.assert_array_equal(p_gpu, p_or)
+    rows, src = synth.loss_patterns(k, m, r, G, 5 + bb, shuffle=True)
+    recv = synth.assemble_received(data, p_or, src)
+    b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+    b, rr, s = gpu_decode(engine, k, m, bb, recv, rows, inplace=True)
+    assert ("gf_stream" in fec.last_kernels()) == streamed
+    np.testing.assert_array_equal(s, s_or)
+    np.testing.assert_array_equal(rr, r_or)
+    np.testing.assert_array_equal(b, b_or)
+
+
 # ------------------------------------------------- non-default launch options
 OPTION_SETS = [
     {"xor_slots": 3, "xor_waves": 3}, {"xor_slots": 4, "xor_waves": 2}, {"xor_waves": 1},
@@ -395,6 +423,8 @@ OPTION_SETS = [
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
     {"stream_ring": 36}, {"host_chunk_mb": 1}, {"const_enc": 0}, {"tile": 0},
     {"tile_depth": 4}, {"tile_pair": 0}, {"stream_static": 0},
+    {"tile_occ2": 1, "tile_depth": 5}, {"tile_occ2": 1, "tile_depth": 6, "tile_pair": 0},
+    {"tile_occ2": 1, "tile_depth": 4, "tile_pair": 0}, {"bsyn": 0}, {"bsyn_depth": 3},
 ]
 
 
@@ -405,7 +435,8 @@ def test_options_parity(tuned_engine, oracle, opts):
     for name, v in opts.items():
         engine.set_option(name, v)
         assert engine.get_option(name) == v
-    for (k, m, bb, r) in [(10, 1, 1352, 1), (32, 4, 1352, 2), (16, 8, 9008, 5), (17, 6, 136, 6)]:
+    for (k, m, bb, r) in [(10, 1, 1352, 1), (32, 4, 1352, 2), (16, 8, 9008, 5), (17, 6, 136, 6),
+                          (128, 16, 9008, 8)]:
         G = 7
         data = synth.group_data(555 + k + m, k, bb, G)
         p_or, rc_or = oracle.encode_batch(k, m, bb, data)
@@ -440,7 +471,7 @@ def test_last_kernels_reports_launches(tuned_engine):
     engine = tuned_engine
     for (k, m, bb, enc, dec) in [
             (10, 1, 1352, "xor_dma_kernel<encode>", "xor_dma_kernel<decode,recovered>"),
-            (32, 4, 1352, "gf_ring_kernel<encode,k32m4>", "gf_stream_kernel<decode>"),
+            (32, 4, 1352, "gf_ring_kernel<encode,k32m4>", "gf_bsyn_kernel<decode,k32m4>"),
             (32, 3, 1352, "gf_stream_kernel<encode>", "gf_stream_kernel<decode>"),
             (16, 4, 1352, "gf_stream_kernel<encode>", "gf_stream_kernel<decode>")]:
         G = 8
@@ -596,7 +627,8 @@ def test_stream_any_small_block(engine, oracle, bb, k, m, r):
     recv = synth.assemble_received(data, p_or, src)
     b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
     b, rr, s = gpu_decode(engine, k, m, bb, recv, rows, inplace=True)
-    assert "gf_stream_kernel<decode" in fec.last_kernels()
+    dec = "gf_bsyn_kernel<decode" if (k, m, bb) == (32, 4, 1352) else "gf_stream_kernel<decode"
+    assert dec in fec.last_kernels()
     np.testing.assert_array_equal(s, s_or)
     np.testing.assert_array_equal(rr, r_or)
     np.testing.assert_array_equal(b, b_or)
@@ -605,10 +637,71 @@ def test_stream_any_small_block(engine, oracle, bb, k, m, r):
     rec = torch.zeros((G, rmax, bb), dtype=torch.uint8, device="cuda")
     rec_rows = torch.zeros((G, rmax), dtype=torch.uint8, device="cuda")
     engine.decode_recovered(k, m, bb, dev(recv), dev(rows), rec, rec_rows)
-    assert "gf_stream_kernel<decode" in fec.last_kernels()
+    assert dec in fec.last_kernels()
     np.testing.assert_array_equal(host(rec_rows), exp_rows)
     mask = exp_rows != 255
     np.testing.assert_array_equal(host(rec)[mask], exp[mask])
+
+
+# ------------------------------------------------- gf_bsyn (compiled (32, 4) decode, B/C)
+@pytest.mark.parametrize("depth", [3, 5, 7])
+@pytest.mark.parametrize("grid", [1, 2, 0])
+def test_bsyn_decode_patterns(tuned_engine, oracle, depth, grid):
+    """Configs B/C's decode (syndromes of every parity row with the compiled (32, 4) code, then
+    the r x r solve, gf_bsyn_kernel) on hand-built receive sets: no loss, 1-4 losses with
+    first / scattered / last parity rows, shuffled arrival (blocks streamed from any slot,
+    odd slots 8 bytes off a 16-byte boundary), a repeated data row (an extra with run-time
+    coefficients), malformed sets (status -3, group unchanged); the grid capped so a wave
+    streams many groups back to back (the next group's blocks are prefetched across the
+    previous group's stores)."""
+    engine = tuned_engine
+    engine.set_option("stream_grid", grid)
+    engine.set_option("bsyn_depth", depth)
+    k, m, bb = 32, 4, 1352
+    rng = np.random.default_rng(300 + depth + grid)
+    G = 24
+    data = synth.group_data(901 + depth + grid, k, bb, G)
+    p_or, _ = oracle.encode_batch(k, m, bb, data)
+
+    def lose(lost, par):
+        keep = [x for x in range(k) if x not in set(lost)]
+        return keep + [k + y for y in par]
+    base = [
+        list(range(k)),
+        lose([5], [0]), lose([0], [3]), lose([31], [2]),
+        lose([3, 4], [0, 1]), lose([0, 31], [2, 3]), lose([7, 19], [1, 3]),
+        lose([1, 2, 3], [0, 1, 2]), lose([8, 16, 24], [1, 2, 3]),
+        lose([0, 1, 2, 3], [0, 1, 2, 3]), lose([28, 29, 30, 31], [0, 1, 2, 3]),
+        lose(sorted(rng.choice(k, 4, replace=False)), [0, 1, 2, 3]),
+    ]
+    dup = list(range(k))                      # row 6 twice, row 5 missing, parity row 2
+    dup[5] = 6
+    dup[20] = k + 2
+    sets = base + [dup]
+    while len(sets) < G - 2:
+        r = int(rng.integers(0, 5))
+        sets.append(lose(sorted(rng.choice(k, r, replace=False)), sorted(rng.choice(m, r, replace=False))))
+    bad1 = lose([3, 4], [1, 1])               # the same parity row twice: singular
+    bad2 = lose([10], [1])
+    bad2[-1] = 200                            # row tag past k + m
+    sets += [bad1, bad2]
+    rows = np.zeros((G, k), np.uint8)
+    src = np.zeros((G, k), np.int16)
+    for g, s in enumerate(sets):
+        s = np.array(s)
+        if g % 2:
+            s = s[rng.permutation(k)]
+        rows[g] = s
+        src[g] = np.where(s < k + m, s, 0)
+    recv = synth.assemble_received(data, p_or, src)
+    ok = np.arange(G) < G - 2
+    s_or = check_decodes(engine, oracle, k, m, bb, recv[ok], rows[ok],
+                         "gf_bsyn_kernel<decode,k32m4>")
+    assert (s_or == 0).all()
+    b, rr, st = gpu_decode(engine, k, m, bb, recv[~ok], rows[~ok], inplace=True)
+    assert st.tolist() == [-3, -3]
+    np.testing.assert_array_equal(rr, rows[~ok])
+    np.testing.assert_array_equal(b, recv[~ok])
 
 
 # ------------------------------------------------- gf_tile (9008-byte blocks, config D)

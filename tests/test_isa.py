@@ -15,11 +15,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = "/opt/rocm/bin/hipcc"
-COUNTED = {"global_load_lds_dwordx4", "buffer_store_dword", "buffer_store_short",
-           "buffer_store_byte"}
+COUNTED = {"global_load_lds_dwordx4", "buffer_load_dwordx4", "buffer_store_dword",
+           "buffer_store_short", "buffer_store_byte"}
+DMA = ("global_load_lds_dwordx4", "buffer_load_dwordx4")   # the latter only as `... lds`
 
 
-@pytest.fixture(scope="module", params=["gf_stream", "gf_tile"])
+@pytest.fixture(scope="module", params=["gf_stream", "gf_tile", "gf_bsyn"])
 def stream_isa(tmp_path_factory, request):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
@@ -49,7 +50,9 @@ def test_only_counted_vmem(stream_isa):
         ops = re.findall(r"^\s+((?:global|buffer|flat|scratch)_\w+)", body, re.M)
         extra = sorted(set(ops) - COUNTED)
         assert not extra, f"{name}: VMEM outside the vmcnt bookkeeping: {extra}"
-        assert "global_load_lds_dwordx4" in ops
+        assert any(d in ops for d in DMA)
+        for line in re.findall(r"^\s+buffer_load_dwordx4[^\n]*", body, re.M):
+            assert line.rstrip().endswith("lds"), f"{name}: register load: {line.strip()}"
 
 
 def test_no_compiler_vmcnt_waits(stream_isa):
