@@ -134,8 +134,9 @@ struct qfec_ctx {
     hipStream_t stream = nullptr;
     qfec::Tune tune;
     // The decode workspace (dcoef, dslots, dnout, dscratch) is one per context.  Calls may
-    // enqueue on any stream, so every use records ws_ev on its stream and a use on another
-    // stream first waits for it: uses of the workspace are ordered across streams.
+    // enqueue on any stream: a use on another stream than the previous use records ws_ev on
+    // that previous stream and waits for it, so uses of the workspace are ordered across
+    // streams (ws_begin / ws_end).
     hipEvent_t ws_ev = nullptr;
     hipStream_t ws_stream = nullptr;
     bool ws_used = false;
@@ -166,18 +167,25 @@ int set_device(qfec_ctx* c) {
 // Order this call's use of the context's decode workspace after the previous use (which
 // may have been enqueued on another stream).  Not while `st` is capturing into a graph:
 // there the calls of one capture are ordered by the capturing stream itself.
+// The event is recorded only when a decode arrives on another stream than the previous
+// one, on that previous stream at that moment: it then follows every kernel already queued
+// there, the previous decode's included.  A decode on the same stream as the last needs no
+// event (stream order), so the common single-stream case queues no marker packet between
+// kernels (each one cost the command processor a few microseconds per call).
 int ws_begin(qfec_ctx* c, hipStream_t st) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     QF_HIP(hipStreamIsCapturing(st, &cs));
     if (cs != hipStreamCaptureStatusNone) return 0;
-    if (c->ws_used && c->ws_stream != st) QF_HIP(hipStreamWaitEvent(st, c->ws_ev, 0));
+    if (c->ws_used && c->ws_stream != st) {
+        QF_HIP(hipEventRecord(c->ws_ev, c->ws_stream));
+        QF_HIP(hipStreamWaitEvent(st, c->ws_ev, 0));
+    }
     return 0;
 }
 int ws_end(qfec_ctx* c, hipStream_t st) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     QF_HIP(hipStreamIsCapturing(st, &cs));
     if (cs != hipStreamCaptureStatusNone) return 0;
-    QF_HIP(hipEventRecord(c->ws_ev, st));
     c->ws_stream = st;
     c->ws_used = true;
     return 0;
@@ -269,6 +277,11 @@ int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
                                       (long long)m * bb, false, st, c->tune));
         return 0;
     }
+    if (qfec::gf_dcol_supported(k, m, bb, c->tune) && ((uintptr_t)d_data & 15) == 0) {
+        QF_HIP(qfec::launch_gf_dcol_encode(d_data, d_par, k, m, bb, G, (long long)m * bb, st,
+                                           c->tune));
+        return 0;
+    }
     if (qfec::gf_tile_supported(k, m, bb, c->tune) && ((uintptr_t)d_data & 15) == 0) {
         QF_HIP(qfec::launch_gf_tile_encode(d_data, d_par, k, m, bb, G, (long long)m * bb, st,
                                            c->tune));
@@ -300,12 +313,19 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
     qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
     const long long tab_gstride = (long long)nchunk * k * std::max(rc, 4);
-    if (qfec::gf_tile_syndrome_supported(k, m, bb, rmax, c->tune) &&
+    const bool dcol = qfec::gf_dcol_supported(k, m, bb, c->tune) && rmax <= 16;
+    if ((dcol || qfec::gf_tile_syndrome_supported(k, m, bb, rmax, c->tune)) &&
         ((uintptr_t)d_blocks & 15) == 0) {
         // compiled (128, 16) code: syndromes, then the r x r solve (reads precede stores
         // within a group, so in place needs no scratch)
         QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc,
                                         rmax, G, st, c->tune, nullptr, true));
+        if (dcol) {
+            QF_HIP(qfec::launch_gf_dcol_syndrome(d_blocks, d_out, w.coef, w.slots, w.nout, cenc,
+                                                 k, m, bb, G, rmax, tab_gstride, (long long)k * bb,
+                                                 st, c->tune));
+            return 0;
+        }
         QF_HIP(qfec::launch_gf_tile_syndrome(d_blocks, d_out, w.coef, w.slots, w.nout, cenc, k,
                                              m, bb, G, rmax, tab_gstride, (long long)k * bb, st,
                                              c->tune));
@@ -383,11 +403,19 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
     if (r) return r;
     if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
     qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
-    if (qfec::gf_tile_syndrome_supported(k, m, bb, rmax, c->tune) &&
+    const bool dcol = qfec::gf_dcol_supported(k, m, bb, c->tune) && rmax <= 16;
+    if ((dcol || qfec::gf_tile_syndrome_supported(k, m, bb, rmax, c->tune)) &&
         ((uintptr_t)d_blocks & 15) == 0) {
         const int nchunk = (rmax + rc - 1) / rc;
         QF_HIP(qfec::launch_decode_prep(d_rows_in, nullptr, d_status, cenc, w, k, m, bb, rc, rmax,
                                         G, st, c->tune, d_rec_rows, true));
+        if (dcol) {
+            QF_HIP(qfec::launch_gf_dcol_syndrome(d_blocks, d_rec, w.coef, nullptr, w.nout, cenc, k,
+                                                 m, bb, G, rmax,
+                                                 (long long)nchunk * k * std::max(rc, 4),
+                                                 (long long)rmax * bb, st, c->tune));
+            return 0;
+        }
         QF_HIP(qfec::launch_gf_tile_syndrome(d_blocks, d_rec, w.coef, nullptr, w.nout, cenc, k, m,
                                              bb, G, rmax, (long long)nchunk * k * std::max(rc, 4),
                                              (long long)rmax * bb, st, c->tune));
@@ -553,7 +581,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"stream_static", &t.stream_static, 0, 1},
         {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_depth", &t.tile_depth, 4, 6}, {"tile_pair", &t.tile_pair, 0, 1},
         {"tile_occ2", &t.tile_occ2, 0, 1},
-        {"bsyn", &t.bsyn, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
+        {"bsyn", &t.bsyn, 0, 1},               {"dcol", &t.dcol, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -578,7 +606,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
         {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"tile", t.tile}, {"tile_grid", t.tile_grid},
         {"tile_depth", t.tile_depth}, {"tile_pair", t.tile_pair}, {"tile_occ2", t.tile_occ2},
-        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth},
+        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb},
     };
@@ -613,7 +641,7 @@ int qfec_ctx_create(int device, qfec_ctx** out) {
 void qfec_ctx_destroy(qfec_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->ws_used) (void)hipEventSynchronize(c->ws_ev);
+    if (c->ws_used) (void)hipStreamSynchronize(c->ws_stream);   // the last use of the workspace
     for (hipStream_t s : {c->stream, c->s_in, c->s_out})
         if (s) (void)hipStreamSynchronize(s);
     if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);

@@ -39,6 +39,8 @@ struct Tune {
     int bsyn = 1;             // (32, 4) x 1352 B decode: compiled syndrome kernel gf_bsyn
                               //   (0: the run-time gf_stream decode)
     int bsyn_depth = 5;       // gf_bsyn: blocks in flight per wave (3..7)
+    int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16
+                              //   rows; 0: gf_tile / gf_tile_syn)
     int host_chunk_mb = 64;   // host-pointer batches: chunk size
 };
 
@@ -94,7 +96,10 @@ constexpr int kNeed = 144;   // u32    bit y: parity row y was received (a syndr
 constexpr int kISlot = 148;  // u8[16] syndrome index i of received parity row y
 constexpr int kERow = 164;   // u8[k]  row tag of extra e
 constexpr int kSinv = 292;   // u8[16][16] Sinv[j][i]: recovered j = sum_i Sinv[j][i] T_i
-constexpr int kBytes = 548;
+constexpr int kRowSlot = 548;  // u8[128] slot holding data row x (255: erased / unchanged group)
+constexpr int kYmap = 676;   // u8[16] parity row y_i of syndrome i (recovery blocks, array order)
+constexpr int kNExt = 692;   // u32    extras to stream after the rows (0: unchanged group)
+constexpr int kBytes = 696;
 }  // namespace syn
 
 // Compact syndrome table of the small-block decode (decode_prep_bsyn, read by gf_bsyn), one
@@ -193,6 +198,18 @@ hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, 
 // Syndrome decode of the compiled (128, 16) code from the syn:: table (gf_tile.hip).
 bool gf_tile_syndrome_supported(int k, int m, int bb, int rmax, const Tune& t);
 hipError_t launch_gf_tile_syndrome(const uint8_t* in, uint8_t* out, const uint8_t* tab,
+                                   const uint8_t* slots, const int32_t* nout,
+                                   const uint8_t* cenc, int k, int m, int bb, long long groups,
+                                   int rmax, long long tab_gstride, long long out_gstride,
+                                   hipStream_t st, const Tune& t);
+
+// One wave per column tile computing all 16 rows (gf_dcol.hip): encode of the compiled
+// (128, 16) x 9008-byte code, and its syndrome decode from the syn:: table.
+bool gf_dcol_supported(int k, int m, int bb, const Tune& t);
+hipError_t launch_gf_dcol_encode(const uint8_t* in, uint8_t* out, int k, int m, int bb,
+                                 long long groups, long long out_gstride, hipStream_t st,
+                                 const Tune& t);
+hipError_t launch_gf_dcol_syndrome(const uint8_t* in, uint8_t* out, const uint8_t* tab,
                                    const uint8_t* slots, const int32_t* nout,
                                    const uint8_t* cenc, int k, int m, int bb, long long groups,
                                    int rmax, long long tab_gstride, long long out_gstride,

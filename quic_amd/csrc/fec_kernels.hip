@@ -467,6 +467,9 @@ __device__ __forceinline__ void prep_group(
             // kernel still reads every group's k blocks
             for (int i = lane; i < k; i += 64) tb[syn::kPerm + i] = (uint8_t)i;
             if (lane < 5) ((uint32_t*)(tb + syn::kMask))[lane] = 0;   // mask and need
+            // gf_dcol: every row position a zero block, no extras
+            for (int x = lane; x < 128; x += 64) tb[syn::kRowSlot + x] = 255;
+            if (lane == 0) *(uint32_t*)(tb + syn::kNExt) = 0;
         }
         if (ro && ro != rg)
             for (int i = lane; i < k; i += 64) ro[i] = rowl[i];
@@ -556,6 +559,12 @@ __device__ __forceinline__ void prep_group(
             }
             ne += __popcll(msk);
         }
+        // gf_dcol: the slot of each data row (255: erased), the parity row of each syndrome,
+        // the count of extras
+        for (int x = lane; x < 128; x += 64)
+            tb[syn::kRowSlot + x] = x < k && present[x] ? (uint8_t)(present[x] - 1) : (uint8_t)255;
+        if (lane < n) tb[syn::kYmap + lane] = (uint8_t)(rowl[recpos[lane]] - k);
+        if (lane == 0) *(uint32_t*)(tb + syn::kNExt) = (uint32_t)ne;
         uint32_t need = 0;
         for (int i = 0; i < n; ++i) need |= 1u << (rowl[recpos[i]] - k);
         if (lane < n) tb[syn::kISlot + rowl[recpos[lane]] - k] = (uint8_t)lane;

@@ -425,6 +425,7 @@ OPTION_SETS = [
     {"tile_depth": 4}, {"tile_pair": 0}, {"stream_static": 0},
     {"tile_occ2": 1, "tile_depth": 5}, {"tile_occ2": 1, "tile_depth": 6, "tile_pair": 0},
     {"tile_occ2": 1, "tile_depth": 4, "tile_pair": 0}, {"bsyn": 0}, {"bsyn_depth": 3},
+    {"dcol": 0}, {"dcol": 0, "tile_occ2": 1, "tile_depth": 5},
 ]
 
 
@@ -606,6 +607,54 @@ def test_config_c_shard_round_trip(engine, oracle):
     torch.cuda.empty_cache()
 
 
+# ------------------------------------------------- config D at its production size
+def test_config_d_full_size_round_trip(engine, oracle):
+    """BASELINE.json configs[4]: 65,536 groups of (128 + 16) x 9000 B (bb 9008), 8 data
+    blocks lost per group and a random 8-subset of the parity rows received, decoded in the
+    recovered-blocks layout (the bench default; 165 GB resident).  At this size every
+    workgroup of the default grid streams 256 groups x 128 blocks through its 32-bit
+    counters and the re-read tail.  Every recovered block equals its original; sampled
+    groups match the oracle byte for byte, parity and recovered blocks."""
+    import torch
+    k, m, bb, r, G = 128, 16, 9008, 8, 65536
+    data = torch.empty((G, k, bb), dtype=torch.uint8, device="cuda")
+    fec.synth_fill(data, seed=4242)
+    parity = torch.zeros((G, m, bb), dtype=torch.uint8, device="cuda")
+    assert engine.encode(k, m, bb, data, parity) == 0
+    assert "gf_dcol" in fec.last_kernels()
+    rows, src = synth.loss_patterns(k, m, r, G, 99)
+    blocks = torch.empty((G, k, bb), dtype=torch.uint8, device="cuda")
+    fec.synth_gather(data, parity, dev(src), blocks, k, m, bb)
+    rec = torch.zeros((G, m, bb), dtype=torch.uint8, device="cuda")
+    rr = torch.zeros((G, m), dtype=torch.uint8, device="cuda")
+    st = torch.full((G,), 9, dtype=torch.int32, device="cuda")
+    engine.decode_recovered(k, m, bb, blocks, dev(rows), rec, rr, status=st)
+    kern = fec.last_kernels()
+    torch.cuda.synchronize()
+    assert "gf_dcol_kernel<decode" in kern, kern
+    assert int(st.abs().max()) == 0
+    got = rr != 255
+    assert bool((got.sum(dim=1) == r).all())
+    # compare in slices of groups (the gathered originals are 4.7 GB)
+    for a in range(0, G, 8192):
+        sl = slice(a, a + 8192)
+        g_got = got[sl]
+        g_idx = torch.arange(a, a + 8192, device="cuda")[:, None].expand(8192, m)[g_got]
+        assert torch.equal(rec[sl][g_got], data[g_idx, rr[sl].long()[g_got]]), a
+    sample = [0, 255, 256, 40961, G - 1]   # first/last groups of a workgroup's stream
+    d_np = host(data[sample])
+    p_or, _ = oracle.encode_batch(k, m, bb, d_np)
+    np.testing.assert_array_equal(host(parity[sample]), p_or)
+    recv = synth.assemble_received(d_np, p_or, src[sample])
+    b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows[sample])
+    exp, exp_rows = expected_recovered(k, m, bb, rows[sample], b_or, r_or, s_or)
+    np.testing.assert_array_equal(host(rr[sample]), exp_rows)
+    mask = exp_rows != 255
+    np.testing.assert_array_equal(host(rec[sample])[mask], exp[mask])
+    del data, parity, blocks, rec
+    torch.cuda.empty_cache()
+
+
 # ------------------------------------------------- gf_stream at other block sizes
 @pytest.mark.parametrize("bb", [1344, 1000, 520, 136, 2048, 8, 1352])
 @pytest.mark.parametrize("k,m,r", [(32, 4, 2), (10, 3, 3), (6, 8, 5)])
@@ -705,14 +754,24 @@ def test_bsyn_decode_patterns(tuned_engine, oracle, depth, grid):
 
 
 # ------------------------------------------------- gf_tile (9008-byte blocks, config D)
+D_KERNELS = {1: ("gf_dcol_kernel<encode,k128m16>", "gf_dcol_kernel<decode,k128m16>"),
+             0: ("gf_tile_kernel<encode,k128m16", "gf_tile_syn_kernel<decode,k128m16>")}
+
+
+@pytest.mark.parametrize("dcol", [1, 0])
 @pytest.mark.parametrize("depth", [4, 6, "6p"])
 @pytest.mark.parametrize("grid", [1, 3, 0])
 @pytest.mark.parametrize("k,m,r", [(128, 16, 8), (128, 16, 13), (40, 16, 16), (16, 6, 4)])
-def test_tile_many_groups_per_workgroup(tuned_engine, oracle, depth, grid, k, m, r):
+def test_tile_many_groups_per_workgroup(tuned_engine, oracle, depth, grid, k, m, r, dcol):
     """Config D's kernels with the grid capped so one workgroup streams several groups back
-    to back (the DMA prefetch crosses group boundaries and the previous group's stores sit
-    in the vmcnt count); every third group has no loss."""
+    to back (the DMA prefetch crosses group / unit boundaries and the previous group's stores
+    sit in the vmcnt count); every third group has no loss.  dcol = 1: gf_dcol (one wave
+    per column tile, units of (group, tile)); dcol = 0: gf_tile / gf_tile_syn (depth
+    options)."""
+    if dcol and depth != 6:
+        pytest.skip("gf_dcol has no depth options")
     engine = tuned_engine
+    engine.set_option("dcol", dcol)
     engine.set_option("tile_grid", grid)
     engine.set_option("tile_depth", 6 if depth == "6p" else depth)
     engine.set_option("tile_pair", 1 if depth == "6p" else 0)   # one barrier per 2 blocks
@@ -721,15 +780,14 @@ def test_tile_many_groups_per_workgroup(tuned_engine, oracle, depth, grid, k, m,
     p_or, rc_or = oracle.encode_batch(k, m, bb, data)
     p_gpu, rc = gpu_encode(engine, k, m, bb, data)
     if (k, m) == (128, 16):
-        assert fec.last_kernels().startswith("gf_tile_kernel<encode,k128m16")
+        assert fec.last_kernels().startswith(D_KERNELS[dcol][0])
     assert rc == rc_or == 0
     np.testing.assert_array_equal(p_gpu, p_or)
     rows, src = synth.loss_patterns(k, m, r, G, 71 + grid, shuffle=True)
     rows[::3] = np.arange(k, dtype=rows.dtype)
     src[::3] = np.arange(k, dtype=src.dtype)
     recv = synth.assemble_received(data, p_or, src)
-    dec_kernel = ("gf_tile_syn_kernel<decode,k128m16>" if (k, m) == (128, 16)
-                  else "gf_apply_kernel<decode")
+    dec_kernel = D_KERNELS[dcol][1] if (k, m) == (128, 16) else "gf_apply_kernel<decode"
     check_decodes(engine, oracle, k, m, bb, recv, rows, dec_kernel)
 
 
@@ -758,8 +816,9 @@ def check_decodes(engine, oracle, k, m, bb, recv, rows, dec_kernel):
     return s_or
 
 
+@pytest.mark.parametrize("dcol", [1, 0])
 @pytest.mark.parametrize("grid", [1, 3, 0])
-def test_syndrome_decode_patterns(tuned_engine, oracle, grid):
+def test_syndrome_decode_patterns(tuned_engine, oracle, grid, dcol):
     """Config D's decode (syndromes of the compiled (128, 16) code, then the r x r solve,
     gf_tile_syn_kernel) on hand-built receive sets: no loss, 16 losses, single and scattered
     parity rows, more than 8 losses (two syndrome exchange rounds), a repeated data row (an
@@ -768,6 +827,7 @@ def test_syndrome_decode_patterns(tuned_engine, oracle, grid):
     k + m) are where the reference's result is not defined (its elimination runs on a
     singular bit matrix / reads past its Cauchy matrix): status -3, group left unchanged."""
     engine = tuned_engine
+    engine.set_option("dcol", dcol)
     engine.set_option("tile_grid", grid)
     k, m, bb = 128, 16, 9008
     rng = np.random.default_rng(90 + grid)
@@ -805,8 +865,7 @@ def test_syndrome_decode_patterns(tuned_engine, oracle, grid):
         src[g] = np.where(s < k + m, s, 0)
     recv = synth.assemble_received(data, p_or, src)
     ok = np.array([g not in (7, 8) for g in range(10)])
-    s_or = check_decodes(engine, oracle, k, m, bb, recv[ok], rows[ok],
-                         "gf_tile_syn_kernel<decode,k128m16>")
+    s_or = check_decodes(engine, oracle, k, m, bb, recv[ok], rows[ok], D_KERNELS[dcol][1])
     assert (s_or == 0).all()
     bad = ~ok
     b, rr, st = gpu_decode(engine, k, m, bb, recv[bad], rows[bad], inplace=True)

@@ -20,27 +20,37 @@ COUNTED = {"global_load_lds_dwordx4", "buffer_load_dwordx4", "buffer_store_dword
 DMA = ("global_load_lds_dwordx4", "buffer_load_dwordx4")   # the latter only as `... lds`
 
 
-@pytest.fixture(scope="module", params=["gf_stream", "gf_tile", "gf_bsyn"])
+@pytest.fixture(scope="module", params=["gf_stream", "gf_tile", "gf_bsyn", "gf_dcol"])
 def stream_isa(tmp_path_factory, request):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
     name = request.param
-    out = tmp_path_factory.mktemp("isa") / f"{name}.s"
     src = os.path.join(ROOT, "quic_amd", "csrc", f"{name}.hip")
-    subprocess.run(["python3", os.path.join(ROOT, "tools", "gen_cauchy_const.py")], check=True,
-                   capture_output=True)
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17",
-                    "-mllvm", "-structurizecfg-skip-uniform-regions=true", "-DQFEC_BUILD",
-                    "-I", os.path.join(ROOT, "build", "gen"),
-                    "-I", os.path.join(ROOT, "quic_amd", "csrc"),
-                    "--cuda-device-only", "-S", "-o", str(out), src],
-                   check=True, capture_output=True)
-    text = out.read_text()
+    # the build keeps the assembly its object was made from (Makefile SAVE_ASM); use it when
+    # it is newer than every input, else compile the file here
+    built = os.path.join(ROOT, "build", f"{name}-hip-amdgcn-amd-amdhsa-gfx950.s")
+    csrc = os.path.join(ROOT, "quic_amd", "csrc")
+    inputs = [src] + [os.path.join(csrc, h) for h in ("fec_kernels.h", "gf_bitslice.h", "gf256.h")]
+    inputs += [os.path.join(ROOT, "tools", "gen_cauchy_const.py"), os.path.join(ROOT, "Makefile")]
+    if os.path.exists(built) and all(os.path.getmtime(built) >= os.path.getmtime(f)
+                                     for f in inputs):
+        out = built
+    else:
+        out = str(tmp_path_factory.mktemp("isa") / f"{name}.s")
+        subprocess.run(["python3", os.path.join(ROOT, "tools", "gen_cauchy_const.py")],
+                       check=True, capture_output=True)
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17",
+                        "-mllvm", "-structurizecfg-skip-uniform-regions=true", "-DQFEC_BUILD",
+                        "-I", os.path.join(ROOT, "build", "gen"), "-I", csrc,
+                        "--cuda-device-only", "-S", "-o", out, src],
+                       check=True, capture_output=True)
+    with open(out) as f:
+        text = f.read()
     bodies = {}
-    for m in re.finditer(r"^(_ZN4qfec\d+gf_\w+?_kernel\w+):", text, re.M):   # every kernel
+    for m in re.finditer(r"^(_ZN4qfec(?:12_GLOBAL__N_1)?\d+gf_\w+?_kernel\w+):", text, re.M):   # every kernel
         end = text.index(".Lfunc_end", m.end())
         bodies[m.group(1)] = text[m.end():end]
-    assert len(bodies) >= 3, "expected the encode and decode instantiations"
+    assert len(bodies) >= 2, "expected the encode and decode instantiations"
     assert not re.search(r"\.private_segment_fixed_size:\s+[1-9]", text), "register spills"
     return bodies
 
