@@ -60,6 +60,8 @@ def block_bytes(payload):
 def workload_label(name, k, m, payload, r, groups_total, world):
     kind = "XOR parity" if m == 1 else "GF(2^8)"
     lab = f"{groups_total} x ({k}+{m}) x {payload}B {kind}, {r}-loss decode"
+    if name == "P":
+        lab = f"QuicR preset FEC_{k}_{m}: " + lab
     if world > 1:
         lab += f", {world} GPUs"
     return f"{name}: {lab}"
@@ -384,6 +386,10 @@ def main():
                     help="groups per GPU (A/B/D) or in total (C); default: the BASELINE size")
     ap.add_argument("--losses", type=int, default=None,
                     help="data blocks lost per group (default: the workload's)")
+    ap.add_argument("--preset", default=None, metavar="K,M",
+                    help="a QuicR FEC preset instead of the BASELINE codes (quic_fec_group.cc:"
+                         "22-82: 5,5 10,10 10,15 10,20 15,15 250,5): 65,536 groups of (K + M) x "
+                         "1350 B, min(K, M) // 2 losses unless --losses")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-groups", type=int, default=None,
                     help="groups per thread in the CPU sample (default: about 8 MB of data "
@@ -408,6 +414,9 @@ def main():
                          "qfec_decode_batch writes them into their slots of a [G][k][bb] "
                          "buffer (cauchy_256_decode layout, out of place)")
     ap.add_argument("--host-steps", type=int, default=3)
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch each step's kernels one by one instead of replaying the step "
+                         "captured once in a HIP graph")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine launch option (qfec_ctx_set_option), for A/B experiments")
     args = ap.parse_args()
@@ -442,6 +451,9 @@ def main():
     from quic_amd import fec, shard, synth
     wname = args.workload or ("A" if world == 1 else "C")
     k, m, payload, r, groups_dflt, strong = WORKLOADS[wname]
+    if args.preset:
+        k, m = (int(x) for x in args.preset.split(","))
+        wname, payload, r, groups_dflt, strong = "P", 1350, max(1, min(k, m) // 2), 65536, False
     if args.losses is not None:
         r = args.losses
     groups_arg = args.groups if args.groups is not None else groups_dflt
@@ -506,6 +518,36 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
+    # The step (its encode and decode launches, every argument fixed) captured once in a HIP
+    # graph and replayed: the same kernels with the same work, without the per-call host path.
+    # Falls back to eager launches if capture is refused.
+    graph, launch_mode = None, "eager launches"
+    if not args.no_graph:
+        try:
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side):
+                    step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g.replay()
+            torch.cuda.synchronize(dev)
+            graph, launch_mode = g, "HIP graph replay of the captured step"
+        except Exception as e:   # the bench still runs, eagerly; the reason is reported
+            launch_mode = f"eager launches (graph capture failed: {e!r:.120})"
+            torch.cuda.synchronize(dev)
+
+    def timed_step():
+        if graph is not None:
+            graph.replay()
+        else:
+            step()
+
+    for _ in range(2):
+        timed_step()
+    torch.cuda.synchronize(dev)
+
     # ---- timed region: barrier + sync on both sides, K steps, nothing else on the stream
     # (no timing events: they cost A about 3 % of its step time)
     if world > 1:
@@ -513,7 +555,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        timed_step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -595,6 +637,8 @@ def main():
 
     phase = "encode" if enc_ms >= dec_ms else "decode"
     traffic, traffic_src = pmc_traffic("B" if wname == "C" else wname, phase, G)
+    if wname == "P":
+        traffic, traffic_src = None, None
     if phase == "encode":
         dom = (kernels["encode"], enc_gbs, enc_bytes, enc_ms)
     else:
@@ -663,6 +707,7 @@ def main():
                 "decode_layout": args.decode_layout, "loss_mode": args.loss_mode,
                 "parity_rows": args.parity,
                 "options": args.opt,
+                "launch": launch_mode,
             },
             "roofline": {
                 "bound": "hbm",

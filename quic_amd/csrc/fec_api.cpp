@@ -271,7 +271,8 @@ int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     const uint8_t* tab = nullptr;
     int rcode = get_enc_table(c, k, m, rc, &tab);
     if (rcode) return rcode;
-    if (m <= rc && qfec::gf_stream_supported(k, m, bb, rc, false, c->tune) &&
+    // gf_stream: m <= 8 as one chunk of m outputs, m > 8 in chunks of 8 (rc == 8)
+    if ((m <= rc || rc == 8) && qfec::gf_stream_supported(k, m, bb, rc, false, c->tune) &&
         ((uintptr_t)d_data & 15) == 0) {
         QF_HIP(qfec::launch_gf_stream(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc, 0, 0,
                                       (long long)m * bb, false, st, c->tune));
@@ -343,13 +344,25 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc, rmax,
                                     G, st, c->tune));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
-    if (nchunk == 1 && qfec::gf_stream_supported(k, m, bb, rc, true, c->tune) &&
+    if (qfec::gf_stream_supported(k, m, bb, rc, true, c->tune) &&
         ((uintptr_t)d_blocks & 15) == 0) {
-        // a group's stores follow all of its reads: in place needs no scratch
         const int rcp = std::max(rc, 4);
-        QF_HIP(qfec::launch_gf_stream(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G, rc,
-                                      rmax, (long long)nchunk * k * rcp, (long long)k * bb, true,
-                                      st, c->tune));
+        if (nchunk == 1 || d_out != d_blocks) {
+            // one chunk: a group's stores follow all of its reads, so in place needs no
+            // scratch; several chunks (units on different waves) write out of place only
+            QF_HIP(qfec::launch_gf_stream(d_blocks, d_out, w.coef, w.slots, w.nout, k, m, bb, G,
+                                          rc, rmax, (long long)nchunk * k * rcp,
+                                          (long long)k * bb, true, st, c->tune));
+            return 0;
+        }
+        // in place with several chunks: the recovered blocks go to scratch first, then to
+        // their slots (a later chunk reads slots an earlier one would have overwritten)
+        QF_HIP(c->dscratch.ensure((size_t)G * rmax * bb));
+        QF_HIP(qfec::launch_gf_stream(d_blocks, (uint8_t*)c->dscratch.p, w.coef, nullptr, w.nout,
+                                      k, m, bb, G, rc, rmax, (long long)nchunk * k * rcp,
+                                      (long long)rmax * bb, true, st, c->tune));
+        QF_HIP(qfec::launch_scatter_recovered((const uint8_t*)c->dscratch.p, d_out, w, k, bb,
+                                              rmax, G, st));
         return 0;
     }
     if (nchunk > 1 && d_out == d_blocks) {
@@ -431,12 +444,13 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
     QF_HIP(qfec::launch_decode_prep(d_rows_in, nullptr, d_status, cenc, w, k, m, bb, rc, rmax, G,
                                     st, c->tune, d_rec_rows));
     if (bb % 8 != 0 || k + m > 256) return 0;   // every group is a no-op or status -1
-    if (rmax <= rc && qfec::gf_stream_supported(k, m, bb, rc, true, c->tune) &&
+    if (qfec::gf_stream_supported(k, m, bb, rc, true, c->tune) &&
         ((uintptr_t)d_blocks & 15) == 0) {
         const int rcp = std::max(rc, 4);
+        const int nchunk = (rmax + rc - 1) / rc;
         QF_HIP(qfec::launch_gf_stream(d_blocks, d_rec, w.coef, nullptr, w.nout, k, m, bb, G, rc,
-                                      rmax, (long long)k * rcp, (long long)rmax * bb, true, st,
-                                      c->tune));
+                                      rmax, (long long)nchunk * k * rcp, (long long)rmax * bb,
+                                      true, st, c->tune));
         return 0;
     }
     QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, d_rec, w, k, m, bb, G, rc, rmax, st,
@@ -581,7 +595,8 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"stream_static", &t.stream_static, 0, 1},
         {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_depth", &t.tile_depth, 4, 6}, {"tile_pair", &t.tile_pair, 0, 1},
         {"tile_occ2", &t.tile_occ2, 0, 1},
-        {"bsyn", &t.bsyn, 0, 1},               {"dcol", &t.dcol, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
+        {"bsyn", &t.bsyn, 0, 1},               {"dcol", &t.dcol, 0, 1},
+        {"dcol_cache", &t.dcol_cache, 0, 3},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -606,7 +621,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
         {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"tile", t.tile}, {"tile_grid", t.tile_grid},
         {"tile_depth", t.tile_depth}, {"tile_pair", t.tile_pair}, {"tile_occ2", t.tile_occ2},
-        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol},
+        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol}, {"dcol_cache", t.dcol_cache},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb},
     };

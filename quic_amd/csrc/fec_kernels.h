@@ -41,6 +41,9 @@ struct Tune {
     int bsyn_depth = 5;       // gf_bsyn: blocks in flight per wave (3..7)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16
                               //   rows; 0: gf_tile / gf_tile_syn)
+    int dcol_cache = 2;       // gf_dcol cache policy: encode 0 non-temporal loads and stores,
+                              //   1 cached loads, 2 / 3 cached loads and stores; decode
+                              //   (stores plain) non-temporal loads for 0 / 2, cached 1 / 3
     int host_chunk_mb = 64;   // host-pointer batches: chunk size
 };
 

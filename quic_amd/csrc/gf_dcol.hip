@@ -62,9 +62,10 @@ __device__ __forceinline__ void dc_wait_vmcnt() {
 // 16 bytes per lane from buffer rs at voff into LDS at lds + 16 * lane (nt).  Lanes whose
 // offset lies past the buffer's range load zeros.  (Device only: in a lambda the builtin
 // would void the kernel's host stub.)
+template <int AUX>
 __device__ __forceinline__ void dc_dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds, uint32_t voff) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, QD_LPTR(lds), 16, voff, 0, 0, 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, QD_LPTR(lds), 16, voff, 0, 0, AUX);
 #else
     (void)rs, (void)lds, (void)voff;
 #endif
@@ -121,7 +122,10 @@ struct DcShape {
                   NDMA * 64 == 8 * SEGL, "shape");
 };
 
-template <int S, int D, bool DECODE>
+// CACHE: bit 0 = the DMA loads are plain (cached) instead of non-temporal, bit 1 = the
+// stores are plain instead of non-temporal.  Neighbouring tiles' 256-byte envelopes share
+// cache lines, which a non-temporal load evicts first.
+template <int S, int D, bool DECODE, int CACHE>
 __global__ __launch_bounds__(kDcWaves * 64, 2) void gf_dcol_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout,
@@ -199,8 +203,9 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void gf_dcol_kernel(
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void*)(un.src + boff), 0, nrec, 0x00020000);
         uint8_t* dst = ring + iss_off;
-        dc_dma16(rs, dst, v0);
-        dc_dma16(rs, dst + 1024, v1);
+        constexpr int LAUX = (CACHE & 1) ? 0 : 2;
+        dc_dma16<LAUX>(rs, dst, v0);
+        dc_dma16<LAUX>(rs, dst + 1024, v1);
         iss_off += BUFB;
         if (iss_off == NBUF * BUFB) iss_off = 0;
     };
@@ -358,7 +363,7 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void gf_dcol_kernel(
         // one output block: 8 sub-row dword stores, plus the tail word's 16-bit store in the
         // last tile (S % 4 == 2)
         static_assert(S % 4 == 2, "the tail word of a sub-row holds 2 bytes");
-        constexpr int SAUX = DECODE ? 0 : 2;   // the encode's dense parity stream: nt
+        constexpr int SAUX = (CACHE & 2) ? 0 : 2;
         auto store_out = [&](uint8_t* dst, bool on, const uint32_t (&o)[8])
                              __attribute__((always_inline)) {
             const __amdgpu_buffer_rsrc_t rs =
@@ -524,9 +529,19 @@ hipError_t launch_gf_dcol_encode(const uint8_t* in, uint8_t* out, int k, int m, 
     const long long waves = (long long)grid * kDcWaves;
     if ((groups * SH::NT + waves - 1) / waves >= (1LL << 31)) return hipErrorInvalidValue;
     note_kernel("gf_dcol_kernel<encode,k128m16>");
-    qlaunch((gf_dcol_kernel<kDcolS, D, false>), dim3(grid), dim3(kDcWaves * 64), lds, st, in,
-            out, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (const int32_t*)nullptr,
-            (const uint8_t*)nullptr, groups, 0, groups * (long long)k * bb, 0LL, out_gstride);
+#define QD_ENC(C)                                                                              \
+    qlaunch((gf_dcol_kernel<kDcolS, D, false, C>), dim3(grid), dim3(kDcWaves * 64), lds, st, \
+            in, out, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (const int32_t*)nullptr, \
+            (const uint8_t*)nullptr, groups, 0, groups * (long long)k * bb, 0LL, out_gstride)
+    // dcol_cache 0: non-temporal loads and stores, 1: cached loads, >= 2: cached loads and
+    // stores (default: the parity's partial cache lines at tile edges merge in L2 instead of
+    // going to HBM twice; D encode 21.7 -> 16.5 ms)
+    switch (t.dcol_cache) {
+        case 0: QD_ENC(0); break;
+        case 1: QD_ENC(1); break;
+        default: QD_ENC(3); break;
+    }
+#undef QD_ENC
     return hipGetLastError();
 }
 
@@ -548,9 +563,14 @@ hipError_t launch_gf_dcol_syndrome(const uint8_t* in, uint8_t* out, const uint8_
     const long long waves = (long long)grid * kDcWaves;
     if ((groups * SH::NT + waves - 1) / waves >= (1LL << 31)) return hipErrorInvalidValue;
     note_kernel("gf_dcol_kernel<decode,k128m16>");
-    qlaunch((gf_dcol_kernel<kDcolS, D, true>), dim3(grid), dim3(kDcWaves * 64), lds, st, in,
-            out, tab, slots, nout, cenc, groups, rmax, groups * (long long)k * bb, tab_gstride,
-            out_gstride);
+    // decode stores are plain; loads non-temporal (dcol_cache 0, 2) or cached (1, 3)
+#define QD_DEC(C)                                                                              \
+    qlaunch((gf_dcol_kernel<kDcolS, D, true, C>), dim3(grid), dim3(kDcWaves * 64), lds, st,  \
+            in, out, tab, slots, nout, cenc, groups, rmax, groups * (long long)k * bb,          \
+            tab_gstride, out_gstride)
+    if (t.dcol_cache & 1) QD_DEC(3);
+    else QD_DEC(2);
+#undef QD_DEC
     return hipGetLastError();
 }
 

@@ -79,11 +79,18 @@ constexpr int kMirror = 2;                 // mirrored slots: a block (<= 2 KiB 
 // from cauchy_const.h at compile time.  The block loop is then fully unrolled and every
 // 8x8 bit expansion folds into its straight-line XORs: no coefficient loads and no scalar
 // nibble dispatch (about 9 scalar instructions per nibble in the run-time form).
+//
+// Units: a group's outputs are cut into nchunk chunks of RC (encode m > 8, decode rmax > 8);
+// a unit is one (group, chunk) and streams the whole group (the chunks of one group run on
+// neighbouring waves, so the re-reads hit L2).  Groups whose byte offset is 8 mod 16 (odd k
+// with bb = 8 mod 16: the reference's (5, 5) and (15, 15) presets at 1352-byte blocks) are
+// streamed from the 16-byte boundary below them, their blocks 8 bytes into the stream.
 template <int RC, int S, bool DECODE, int RCPT = (RC < 4 ? 4 : RC), int KC = 0>
 __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
-    int k, int m, int rmax, long long coef_gstride, long long out_gstride, int R, int s_rt) {
+    int k, int m, int rmax, long long coef_gstride, long long out_gstride, int R, int s_rt,
+    int nchunk) {
     static_assert(KC == 0 || (!DECODE && RC >= 2 && RC <= 6 && S > 0),
                   "compile-time codes: encode, m <= 6, fixed block size");
     static_assert(S <= 256, "one column word of each sub-row per lane");
@@ -102,13 +109,15 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const int RB = R * 1024;
     uint8_t* ring = smem + (size_t)w * (R + kMirror) * 1024;
     const long long W = (long long)gridDim.x * kStreamWaves;
-    const long long g0 = (long long)blockIdx.x * kStreamWaves + w;
-    if (g0 >= groups) return;
+    const long long g0 = (long long)blockIdx.x * kStreamWaves + w;   // the wave's first unit
+    const long long NU = groups * nchunk;
+    if (g0 >= NU) return;
     const long long cnt =   // wave-uniform, kept in SGPRs (the division runs on the VALU)
-        __builtin_amdgcn_readfirstlane((int)((groups - 1 - g0) / W + 1));   // groups of this wave
+        __builtin_amdgcn_readfirstlane((int)((NU - 1 - g0) / W + 1));   // units of this wave
     if constexpr (KC > 0) k = KC;
     const int gb = k * BB;
-    const int NP = (gb + 1023) >> 10;                  // pieces per group
+    const int skew8 = (gb & 15) ? 8 : 0;               // groups may start 8 mod 16
+    const int NP = (gb + skew8 + 1023) >> 10;          // pieces per unit
     const int c = lane < NW ? lane : NW - 1;           // idle lanes shadow the last word
 
     // ---- issue side (wave-uniform): next piece iss_p of the stream, into slot iss_slot
@@ -117,11 +126,19 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const int total = (int)cnt * NP;
     int vm = 0;                                        // VMEM instructions issued
     uint32_t vmv = 0;                                  // lane s: vm index of slot s's last write
-    const uint8_t* isrc = in + g0 * gb;
-    const long long istride = W * gb;
+    // the 16-byte aligned start of unit u's group, and its last 16-byte chunk (clamp)
+    long long iss_u = g0;
+    auto unit_src = [&](long long u, int& last) -> const uint8_t* {
+        const long long a = (u / nchunk) * (long long)gb;
+        const int sk = (int)(a & 15);
+        last = (sk + gb - 1) & ~15;
+        return in + (a - sk);
+    };
+    int ilast = 0;
+    const uint8_t* isrc = unit_src(g0, ilast);
 
     auto issue_one = [&]() {
-        const int off = min(iss_p * 1024 + lane * 16, gb - 16);   // last piece: clamp inside
+        const int off = min(iss_p * 1024 + lane * 16, ilast);   // last piece: clamp inside
         __builtin_amdgcn_global_load_lds(QS_GPTR(isrc + off), QS_LPTR(ring + iss_slot * 1024),
                                          16, 0, 2);
         ++vm;
@@ -135,7 +152,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
         if (++iss_slot == R) iss_slot = 0;
         if (++iss_p == NP) {
             iss_p = 0;
-            isrc += istride;
+            iss_u += W;
+            isrc = unit_src(iss_u, ilast);
         }
     };
     // top the ring up: every piece from `head` on stays, the rest of the R slots refill
@@ -189,11 +207,15 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     int gslot0 = 0;                                    // its slot
 #pragma unroll 1
     for (long long i = 0; i < cnt; ++i) {
-        const long long g = g0 + i * W;
-        int n = DECODE ? nout[g] : RC;   // encode: RC == m
+        const long long u = g0 + i * W;
+        const long long g = u / nchunk;
+        const int ch = (int)(u - g * nchunk);            // output chunk: outputs ch * RC + j
+        const int sk = (int)((g * gb) & 15);             // the group's bytes start sk into its stream
+        int n = (DECODE ? nout[g] : m) - ch * RC;
         n = n > RC ? RC : n;
         if (n > 0) {
-            const uint32_t* cw = (const uint32_t*)(coef + (DECODE ? g * coef_gstride : 0));
+            const uint32_t* cw = (const uint32_t*)(coef + (DECODE ? g * coef_gstride : 0) +
+                                                   (long long)ch * k * RCPT);
             uint32_t acc[RC][8];
 #pragma unroll
             for (int j = 0; j < RC; ++j)
@@ -202,7 +224,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
             // Block x + 1's LDS reads are issued before block x is combined (software
             // pipeline); the ring keeps every piece from block x's first on, so block x's
             // pieces are not refilled while its reads may still be in flight.
-            uint32_t bpos = (uint32_t)gslot0 * 1024u;          // ring position of block x
+            uint32_t bpos = (uint32_t)gslot0 * 1024u + (uint32_t)sk;   // ring position of block x
             uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
             fill(gbase);
             wait_block(bpos);
@@ -223,7 +245,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                 const int x = xc;
                 const uint32_t bn = next_pos(bpos);
                 if (x + 1 < k) {
-                    fill(gbase + ((x * BB) >> 10));
+                    fill(gbase + ((sk + x * BB) >> 10));
                     wait_block(bn);
                     read_block(bn, nlo, nhi);
                 }
@@ -256,12 +278,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                 expand_wz(v);
 #pragma unroll
                 for (int j = 0; j < RC; ++j) {
-                    if (!DECODE && j == 0) {
+                    if (!DECODE && j == 0 && ch == 0) {
                         // encode row 0 is P0, all coefficients 1 (cauchy_256.cpp:1519-1523):
                         // a plain XOR, no scalar nibble dispatch
 #pragma unroll
                         for (int r = 0; r < 8; ++r) acc[0][r] ^= v.W[r];
-                    } else if (!DECODE || j < n) {
+                    } else if (j < n) {
                         const uint32_t cf = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
                         apply_nibble<0>(acc[j], cf & 15u, v);
                         apply_nibble<4>(acc[j], cf >> 4, v);
@@ -298,7 +320,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
 #pragma unroll
             for (int j = 0; j < RC; ++j) {
                 if (j < n) {
-                    const int oslot = (DECODE && slots) ? sload_u8(slots, g * rmax + j) : j;
+                    const int jo = ch * RC + j;
+                    const int oslot = (DECODE && slots) ? sload_u8(slots, g * rmax + jo) : jo;
                     uint8_t* dst = out + g * out_gstride + (long long)oslot * BB;
                     const __amdgpu_buffer_rsrc_t rs =
                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, (unsigned)BB, 0x00020000);
@@ -641,7 +664,7 @@ bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& 
     if (!t.stream) return false;
     if (bb % 8 != 0 || bb < 8 || bb > 2048) return false;   // s <= 256: a word per lane
     if (rc != 2 && rc != 4 && rc != 8) return false;
-    if (((long long)k * bb) % 16 != 0 || (long long)k * bb < 16) return false;
+    if ((long long)k * bb < 16) return false;   // groups 8 mod 16 apart stream skewed
     if (t.stream_ring < gf_stream_min_ring(bb)) return false;   // gf_apply instead
     return true;
 }
@@ -659,7 +682,11 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     const size_t lds = (size_t)kStreamWaves * (R + kMirror) * 1024;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int per_cu = (int)((160 * 1024) / lds);
-    const long long want = (groups + kStreamWaves - 1) / kStreamWaves;
+    // units: (group, chunk of rc outputs); encode chunks of 8 for m > 8 (m <= 8: one chunk
+    // of exactly m outputs), decode chunks of rc for rmax > rc
+    const int nchunk = decode ? (rmax + rc - 1) / rc : (m <= 8 ? 1 : (m + 7) / 8);
+    const long long units = groups * nchunk;
+    const long long want = (units + kStreamWaves - 1) / kStreamWaves;
     long long cap = (long long)t.cus * per_cu;
     if (t.stream_grid > 0) cap = t.stream_grid;          // tests: many groups per wave
     const unsigned grid = (unsigned)std::min<long long>(want, cap);
@@ -668,13 +695,13 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     // the wave's 32-bit piece counters: cnt * NP, and (gf_ring) cnt groups
     {
         const long long waves = (long long)grid * kStreamWaves;
-        const long long np = ((long long)k * bb + 1023) / 1024;
-        if ((groups + waves - 1) / waves * np >= (1LL << 31)) return hipErrorInvalidValue;
+        const long long np = ((long long)k * bb + 8 + 1023) / 1024;
+        if ((units + waves - 1) / waves * np >= (1LL << 31)) return hipErrorInvalidValue;
     }
 #define QS_GO(RCV, SV, DEC, RCPV, KCV)                                                        \
     qlaunch((gf_stream_kernel<RCV, SV, DEC, RCPV, KCV>), dim3(grid), dim3(threads), \
                        lds, st, in, out, coef, slots, nout, groups, k, m, rmax, coef_gstride,   \
-                       out_gstride, R, s)
+                       out_gstride, R, s, nchunk)
 #define QS_DEC(SV)                                        \
     switch (rc) {                                         \
         case 2: QS_GO(2, SV, true, 4, 0); break;          \
@@ -692,11 +719,12 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         case 6: QS_GO(6, SV, false, 8, 0); break;         \
         case 7: QS_GO(7, SV, false, 8, 0); break;         \
         case 8: QS_GO(8, SV, false, 8, 0); break;         \
-        default: return hipErrorInvalidValue;             \
+        default: QS_GO(8, SV, false, 8, 0); break;        \
     }
     // the static ring schedule is used for the encode only: its rolled decode measured
     // slower than gf_stream's (0.644 vs 0.619 ms on config B)
-    if (t.stream_static && !decode && k == 32 && s == 169 && m == 4 && t.const_enc) {
+    if (t.stream_static && !decode && k == 32 && s == 169 && m == 4 && t.const_enc &&
+        ((long long)k * bb) % 16 == 0) {
         // the fixed B/C shape: compile-time ring schedule (gf_ring_kernel)
         const size_t rlds = (size_t)kRingWaves * RingShape<169>::RB;
         const long long rwant = (groups + kRingWaves - 1) / kRingWaves;
@@ -725,6 +753,7 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         }
     } else {
         if ((rc < 4 ? 4 : rc) != (m <= 4 ? 4 : 8)) return hipErrorInvalidValue;
+        if (m > 8 && rc != 8) return hipErrorInvalidValue;
         if (s == 169 && t.const_enc && k == 32 && m == 4) {
             // BASELINE configs B/C: the code is fixed at compile time
             note_kernel("gf_stream_kernel<encode,k32m4>");

@@ -425,7 +425,8 @@ OPTION_SETS = [
     {"tile_depth": 4}, {"tile_pair": 0}, {"stream_static": 0},
     {"tile_occ2": 1, "tile_depth": 5}, {"tile_occ2": 1, "tile_depth": 6, "tile_pair": 0},
     {"tile_occ2": 1, "tile_depth": 4, "tile_pair": 0}, {"bsyn": 0}, {"bsyn_depth": 3},
-    {"dcol": 0}, {"dcol": 0, "tile_occ2": 1, "tile_depth": 5},
+    {"dcol": 0}, {"dcol": 0, "tile_occ2": 1, "tile_depth": 5}, {"dcol_cache": 0},
+    {"dcol_cache": 1}, {"dcol_cache": 3},
 ]
 
 
@@ -657,15 +658,13 @@ def test_config_d_full_size_round_trip(engine, oracle):
 
 # ------------------------------------------------- gf_stream at other block sizes
 @pytest.mark.parametrize("bb", [1344, 1000, 520, 136, 2048, 8, 1352])
-@pytest.mark.parametrize("k,m,r", [(32, 4, 2), (10, 3, 3), (6, 8, 5)])
+@pytest.mark.parametrize("k,m,r", [(32, 4, 2), (10, 3, 3), (6, 8, 5), (5, 5, 4), (15, 12, 11)])
 def test_stream_any_small_block(engine, oracle, bb, k, m, r):
     """Groups whose padded blocks are at most 2 KiB (quic_fec_group.cc:344-352 pads to the
     group's longest packet) run the streaming kernel, not gf_apply; bit-exact vs the
     oracle, encode and both decode layouts."""
     import torch
-    if (k * bb) % 16:
-        pytest.skip("odd k with bb % 16 == 8: groups not 16-byte aligned (gf_apply path)")
-    G = 9
+    G = 9   # odd k with bb % 16 == 8: every other group starts 8 bytes off 16
     data = synth.group_data(bb + 17 * k + m, k, bb, G)
     p_or, rc_or = oracle.encode_batch(k, m, bb, data)
     p_gpu, rc = gpu_encode(engine, k, m, bb, data)
@@ -690,6 +689,36 @@ def test_stream_any_small_block(engine, oracle, bb, k, m, r):
     np.testing.assert_array_equal(host(rec_rows), exp_rows)
     mask = exp_rows != 255
     np.testing.assert_array_equal(host(rec)[mask], exp[mask])
+
+
+# ------------------------------------------------- the reference's FEC presets
+PRESETS = [(5, 5), (10, 10), (10, 15), (10, 20), (15, 15), (250, 5)]   # quic_fec_group.cc:22-82
+
+
+@pytest.mark.parametrize("grid", [0, 1])
+@pytest.mark.parametrize("k,m", PRESETS)
+def test_reference_presets_stream(tuned_engine, oracle, k, m, grid):
+    """QuicR's negotiated configurations with 1350-byte payloads (bb = 1352): odd k puts every
+    other group 8 bytes off a 16-byte boundary, m > 8 and more than 8 losses cut the outputs
+    into chunks (units of one group each).  All of them run gf_stream, never gf_apply;
+    bit-exact vs the oracle in every decode layout, with as many losses as the code allows
+    (min(k, m)) and with one; grid 1: one workgroup streams every unit."""
+    import torch
+    engine = tuned_engine
+    engine.set_option("stream_grid", grid)
+    bb, G = 1352, 11
+    data = synth.group_data(9000 + k + m, k, bb, G)
+    p_or, rc_or = oracle.encode_batch(k, m, bb, data)
+    p_gpu, rc = gpu_encode(engine, k, m, bb, data)
+    assert fec.last_kernels().startswith("gf_stream_kernel<encode"), fec.last_kernels()
+    assert rc == rc_or == 0
+    np.testing.assert_array_equal(p_gpu, p_or)
+    for r in (min(k, m), 1):
+        rows, src = synth.loss_patterns(k, m, r, G, 31 + r, shuffle=True)
+        recv = synth.assemble_received(data, p_or, src)
+        s_or = check_decodes(engine, oracle, k, m, bb, recv, rows, "gf_stream_kernel<decode")
+        assert (s_or == 0).all()
+        assert "gf_apply" not in fec.last_kernels()
 
 
 # ------------------------------------------------- gf_bsyn (compiled (32, 4) decode, B/C)
