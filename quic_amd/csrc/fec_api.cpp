@@ -100,6 +100,24 @@ int pow2_at_least(int v) {
 }
 int encode_rc(int m, const qfec::Tune& t) { return std::min(pow2_at_least(m), t.enc_rc); }
 int decode_rc(int rmax) { return std::min(pow2_at_least(rmax), 8); }
+// Encode table rows: gf_apply's chunk (<= 8), or 16 where gf_stream takes 9..16 outputs in
+// one unit (m <= 8: one unit of m outputs; more than 16: chunks of 8; compiled codes read no
+// table)
+int stream_encode_rc(int k, int m, int bb, bool aligned, const qfec::Tune& t) {
+    if (m > 8 && m <= 16 && aligned && qfec::gf_stream_supported(k, m, bb, 16, false, t)) return 16;
+    return encode_rc(m, t);
+}
+// Output chunk of a decode.  gf_stream decodes in units of 8 recovered blocks: a group with
+// at most 8 losses leaves its second unit empty, and empty units read nothing, while one unit
+// of 16 accumulators halves the occupancy for every group ((10, 10) at 5 losses: 0.615 ms
+// with 16, a whole group per unit).  t.stream_rc16 = 1 takes the single 16-block unit.
+int stream_decode_rc(int k, int m, int bb, int rmax, const uint8_t* d_blocks,
+                     const qfec::Tune& t) {
+    if (t.stream_rc16 && rmax > 8 && rmax <= 16 && ((uintptr_t)d_blocks & 15) == 0 &&
+        k + m <= 256 && bb % 8 == 0 && qfec::gf_stream_supported(k, m, bb, 16, true, t))
+        return 16;
+    return decode_rc(rmax);
+}
 
 struct DevBuf {
     void* p = nullptr;
@@ -267,13 +285,13 @@ int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
         QF_HIP(qfec::launch_xor_encode(d_data, d_par, k, bb, G, (long long)m * bb, st, c->tune));
         return m == 1 ? 0 : fail(-1, "unsupported (k + m > 256 or block_bytes % 8 != 0)");
     }
-    const int rc = encode_rc(m, c->tune);
+    const bool aligned = ((uintptr_t)d_data & 15) == 0;
+    const int rc = stream_encode_rc(k, m, bb, aligned, c->tune);
     const uint8_t* tab = nullptr;
     int rcode = get_enc_table(c, k, m, rc, &tab);
     if (rcode) return rcode;
-    // gf_stream: m <= 8 as one chunk of m outputs, m > 8 in chunks of 8 (rc == 8)
     if ((m <= rc || rc == 8) && qfec::gf_stream_supported(k, m, bb, rc, false, c->tune) &&
-        ((uintptr_t)d_data & 15) == 0) {
+        aligned) {
         QF_HIP(qfec::launch_gf_stream(d_data, d_par, tab, nullptr, nullptr, k, m, bb, G, rc, 0, 0,
                                       (long long)m * bb, false, st, c->tune));
         return 0;
@@ -306,7 +324,7 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
         return 0;
     }
     const int rmax = std::min(k, m);
-    const int rc = decode_rc(rmax);
+    const int rc = stream_decode_rc(k, m, bb, rmax, d_blocks, c->tune);
     const int nchunk = (rmax + rc - 1) / rc;
     const uint8_t* cenc = nullptr;
     int r = get_cenc(c, k, m, &cenc);
@@ -410,7 +428,7 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
                                        (uint8_t*)c->dslots.p, k, bb, G, st, c->tune, true));
         return 0;
     }
-    const int rc = decode_rc(rmax);
+    const int rc = stream_decode_rc(k, m, bb, rmax, d_blocks, c->tune);
     const uint8_t* cenc = nullptr;
     int r = get_cenc(c, k, m, &cenc);
     if (r) return r;
@@ -596,7 +614,8 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_depth", &t.tile_depth, 4, 6}, {"tile_pair", &t.tile_pair, 0, 1},
         {"tile_occ2", &t.tile_occ2, 0, 1},
         {"bsyn", &t.bsyn, 0, 1},               {"dcol", &t.dcol, 0, 1},
-        {"dcol_cache", &t.dcol_cache, 0, 3},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
+        {"dcol_cache", &t.dcol_cache, 0, 3},     {"stream_rc16", &t.stream_rc16, 0, 1},
+        {"ring_nt", &t.ring_nt, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -621,7 +640,8 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
         {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"tile", t.tile}, {"tile_grid", t.tile_grid},
         {"tile_depth", t.tile_depth}, {"tile_pair", t.tile_pair}, {"tile_occ2", t.tile_occ2},
-        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol}, {"dcol_cache", t.dcol_cache},
+        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol}, {"dcol_cache", t.dcol_cache}, {"stream_rc16", t.stream_rc16},
+        {"ring_nt", t.ring_nt},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb},
     };
@@ -980,7 +1000,7 @@ int qfec_reserve(qfec_ctx* c, int k, int m, int bb, long long groups) {
     QF_HIP(c->dslots.ensure((size_t)groups));   // m == 1 decode: erased slot per group
     if (m > 1 && k > 1 && k + m <= 256) {
         const uint8_t* t;
-        if ((rc = get_enc_table(c, k, m, encode_rc(m, c->tune), &t))) return rc;
+        if ((rc = get_enc_table(c, k, m, stream_encode_rc(k, m, bb, true, c->tune), &t))) return rc;
     }
     if (m > 1 && k > 1) {
         const uint8_t* t;

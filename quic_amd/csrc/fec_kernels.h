@@ -41,9 +41,12 @@ struct Tune {
     int bsyn_depth = 5;       // gf_bsyn: blocks in flight per wave (3..7)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16
                               //   rows; 0: gf_tile / gf_tile_syn)
-    int dcol_cache = 2;       // gf_dcol cache policy: encode 0 non-temporal loads and stores,
-                              //   1 cached loads, 2 / 3 cached loads and stores; decode
-                              //   (stores plain) non-temporal loads for 0 / 2, cached 1 / 3
+    int dcol_cache = 2;       // gf_dcol cache policy: encode 0 / 1 cached loads and non-temporal
+                              //   stores, 2 / 3 cached loads and stores; decode (stores
+                              //   plain) non-temporal loads for 0 / 2, cached 1 / 3
+    int stream_rc16 = 0;      // gf_stream decode of 9..16 losses as one 16-block unit (0: two
+                              //   units of 8, the second empty for <= 8 losses and skipped)
+    int ring_nt = 1;          // gf_ring (B/C encode) parity stores non-temporal (0: plain)
     int host_chunk_mb = 64;   // host-pointer batches: chunk size
 };
 
@@ -185,6 +188,8 @@ hipError_t launch_xor_dma(const uint8_t* in, uint8_t* out, const uint8_t* eidx,
 
 // Per-wave LDS-ring streaming kernel for bb = 1352, one output chunk (gf_stream.hip).
 bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& t);
+// (k, m) codes whose gf_stream encode is compiled at this block size (no coefficient table)
+bool gf_stream_compiled(int k, int m, int bb);
 hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef,
                             const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
                             long long groups, int rc, int rmax, long long coef_gstride,

@@ -631,6 +631,186 @@ __global__ __launch_bounds__(256) void decode_prep_kernel(
                    rec_rows, k, m, bb, rc, rmax, nchunk, syndrome != 0);
 }
 
+// Decode prep with SIXTEEN lanes per group for small groups with up to 16 erasures (k <= 64:
+// the QuicR presets (5, 5) .. (15, 15) at 1350-byte payloads).  Same bookkeeping, status
+// codes and outputs as prep_group (cauchy_256.cpp:543-575, :791, :1287-1294).  The 16 lanes
+// split the slots (bookkeeping by ballots), then the columns of [S | I] (lane l owns columns
+// l and l + 16 of the group's n x 2n matrix in LDS) for the Gauss-Jordan inverse, then the
+// slots again for the per-slot coefficients.  A wave holds four groups and the lanes of a
+// group exchange data through LDS in program order (one wave: no barrier).  prep_group runs
+// one group per wave through a chain of wave-wide LDS round trips: 270 us for 65,536
+// (10, 10) groups with 5 losses.
+constexpr int kWideLanes = 16;
+__global__ __launch_bounds__(256) void decode_prep_wide_kernel(
+    const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
+    const uint8_t* __restrict__ cenc, uint8_t* __restrict__ coef, uint8_t* __restrict__ slots,
+    int32_t* __restrict__ nout, uint8_t* __restrict__ rec_rows, long long groups, int k, int m,
+    int bb, int rc, int rmax, int nchunk) {
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    constexpr int GPB = 256 / kWideLanes;                       // groups per block
+    __shared__ uint8_t lrows[GPB][64];
+    __shared__ uint8_t lmat[GPB][16][32];                       // [S | I], row-major
+    __shared__ uint8_t llist[GPB][3][16];                       // recpos, y, era
+    extern __shared__ __attribute__((aligned(16))) uint8_t lcenc[];   // m x k
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) gexp[i] = c_gf.exp[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) glog[i] = c_gf.log[i];
+    for (int i = threadIdx.x; i < m * k; i += blockDim.x) lcenc[i] = cenc[i];
+    const long long gfirst = (long long)blockIdx.x * GPB;
+    const int ng = (int)min((long long)GPB, groups - gfirst);
+    for (int i = threadIdx.x; i < ng * k; i += blockDim.x)
+        lrows[i / k][i % k] = rows_in[gfirst * k + i];
+    __syncthreads();
+    const int gl = threadIdx.x / kWideLanes, l = threadIdx.x % kWideLanes;
+    const int seg = (threadIdx.x & 63) / kWideLanes;            // the group's 16 lanes in the wave
+    if (gl >= ng) return;                                       // whole groups: no barrier below
+    const long long g = gfirst + gl;
+    const uint8_t* rg = lrows[gl];
+    uint8_t (*M)[32] = lmat[gl];
+    uint8_t* lrec = llist[gl][0];
+    uint8_t* ly = llist[gl][1];
+    uint8_t* lera = llist[gl][2];
+    auto mul = [&](int a, int b) -> int { return (a && b) ? gexp[glog[a] + glog[b]] : 0; };
+
+    // ---- bookkeeping: slot i = 16 q + l.  isrec: bit i = slot i holds a recovery block;
+    // present: bit r = data row r was received (OR over the group's lanes)
+    uint64_t isrec = 0, present = 0;
+    bool badrow = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = kWideLanes * q + l;
+        const int r = i < k ? rg[i] : 0;
+        const bool rec = i < k && r >= k;
+        if (i < k && r < k) present |= 1ull << r;
+        const uint64_t b = __ballot(rec);
+        isrec |= ((b >> (kWideLanes * seg)) & 0xFFFFull) << (kWideLanes * q);
+    }
+#pragma unroll
+    for (int o = 1; o < kWideLanes; o <<= 1) present |= __shfl_xor(present, o, kWideLanes);
+    const int nrec = __popcll(isrec);
+    const uint64_t kmask = k == 64 ? ~0ull : ((1ull << k) - 1);
+    const uint64_t missing = ~present & kmask;
+    const int nera = __popcll(missing);
+    // entry l of the lists: the l-th recovery slot, its parity row, the l-th erased row
+    int myrec = -1, myera = -1;
+    {
+        uint64_t a = isrec, e = missing;
+        for (int j = 0; j < l && a; ++j) a &= a - 1;
+        for (int j = 0; j < l && e; ++j) e &= e - 1;
+        if (a) myrec = __ffsll((long long)a) - 1;
+        if (e) myera = __ffsll((long long)e) - 1;
+    }
+    const int myy = myrec >= 0 ? rg[myrec] - k : 0;
+    if (l < nrec && l < 16) badrow = myy >= m;
+    const bool anybad = (__ballot(badrow) >> (kWideLanes * seg)) & 0xFFFFull;
+    uint8_t* ro = rows_out ? rows_out + g * k : nullptr;        // null: recovered-blocks layout
+    const uint8_t* rgg = rows_in + g * k;
+    uint8_t* rec = rec_rows ? rec_rows + g * rmax : nullptr;
+    auto finish_unchanged = [&](int st) {
+        if (ro && ro != rgg)
+            for (int i = l; i < k; i += kWideLanes) ro[i] = rg[i];
+        if (rec)
+            for (int j = l; j < rmax; j += kWideLanes) rec[j] = 255;
+        if (l == 0) {
+            nout[g] = 0;
+            if (status) status[g] = st;
+        }
+    };
+    if (nrec == 0) { finish_unchanged(0); return; }                       // :1287-1289
+    if (k + m > 256 || (bb & 7)) { finish_unchanged(-1); return; }        // :1292-1294
+    if (nrec > rmax || nera < nrec || anybad) { finish_unchanged(-3); return; }   // malformed
+    const int n = nrec;                                                   // <= rmax <= 16
+    if (l < n) {
+        lrec[l] = (uint8_t)myrec;
+        ly[l] = (uint8_t)myy;
+        lera[l] = (uint8_t)myera;
+    }
+    wave_sync();
+    // ---- [S | I], S[i][j] = C[y_i][e_j]: lane l fills columns l and l + 16
+    for (int i = 0; i < n; ++i) {
+        const int yi = ly[i];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = l + kWideLanes * h;
+            if (c < 2 * n) M[i][c] = c < n ? lcenc[yi * k + lera[c]] : (uint8_t)(c - n == i);
+        }
+    }
+    wave_sync();
+    // ---- Gauss-Jordan (the lanes own columns; rows through LDS)
+    for (int p = 0; p < n; ++p) {
+        int piv = -1;
+        for (int i = p; i < n && piv < 0; ++i)
+            if (M[i][p]) piv = i;                                 // the same for every lane
+        if (piv < 0) { finish_unchanged(-3); return; }             // singular
+        if (piv != p) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = l + kWideLanes * h;
+                if (c < 2 * n) {
+                    const uint8_t t = M[p][c];
+                    M[p][c] = M[piv][c];
+                    M[piv][c] = t;
+                }
+            }
+            wave_sync();
+        }
+        const int inv = gexp[255 - glog[M[p][p]]];
+        wave_sync();                                              // every lane read M[p][p]
+        int rowp[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = l + kWideLanes * h;
+            rowp[h] = c < 2 * n ? mul(M[p][c], inv) : 0;
+            if (c < 2 * n) M[p][c] = (uint8_t)rowp[h];
+        }
+        for (int i = 0; i < n; ++i) {
+            if (i == p) continue;
+            const int f = M[i][p];                               // before column p changes
+            wave_sync();
+            if (f) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int c = l + kWideLanes * h;
+                    if (c < 2 * n) M[i][c] ^= (uint8_t)mul(f, rowp[h]);
+                }
+            }
+            wave_sync();
+        }
+    }
+    // ---- coefficients per (output j, input slot pos): recovery slot ri: Sinv[j][ri]; data
+    // row x: sum_i Sinv[j][i] C[y_i][x]
+    for (int pos = l; pos < k; pos += kWideLanes) {
+        const bool isr = (isrec >> pos) & 1;
+        const int ri = isr ? __popcll(isrec & ((1ull << pos) - 1)) : -1;
+        const int x = rg[pos];
+        for (int j = 0; j < n; ++j) {
+            int cval;
+            if (isr) {
+                cval = M[j][n + ri];
+            } else {
+                cval = 0;
+                for (int i = 0; i < n; ++i) cval ^= mul(M[j][n + i], lcenc[ly[i] * k + x]);
+            }
+            const int ch = j / rc, jj = j % rc;
+            coef[g * (long long)nchunk * k * (rc < 4 ? 4 : rc) + ((long long)ch * k + pos) *
+                 (rc < 4 ? 4 : rc) + jj] = (uint8_t)cval;
+        }
+    }
+    if (ro && ro != rgg)
+        for (int i = l; i < k; i += kWideLanes) ro[i] = rg[i];
+    wave_sync();
+    if (l < n) {
+        slots[g * rmax + l] = lrec[l];
+        if (ro) ro[lrec[l]] = lera[l];                                     // :791
+    }
+    if (rec)
+        for (int j = l; j < rmax; j += kWideLanes) rec[j] = j < n ? lera[j] : 255;
+    if (l == 0) {
+        nout[g] = n;
+        if (status) status[g] = 0;
+    }
+}
+
 // Decode prep with four LANES per group, for small erasure counts (rmax <= 4, k <= 64: the
 // 1350-byte configs).  Same bookkeeping, status codes and outputs as prep_group above
 // (cauchy_256.cpp:543-575, :791, :1287-1294); the r x r inverse and the per-slot
@@ -1094,6 +1274,13 @@ hipError_t launch_decode_prep(const uint8_t* rows_in, uint8_t* rows_out, int32_t
         return hipGetLastError();
     }
     const int nchunk = (rmax + rc - 1) / rc;
+    if (!syndrome && t.prep_lane && k <= 64 && rmax <= 16 && (long long)m * k <= 16384) {
+        note_kernel("decode_prep_wide_kernel");
+        qlaunch((decode_prep_wide_kernel), dim3((unsigned)((groups + 15) / 16)), dim3(256),
+                (uint32_t)(((size_t)m * k + 15) & ~(size_t)15), st, rows_in, rows_out, status,
+                cenc, w.coef, w.slots, w.nout, rec_rows, groups, k, m, bb, rc, rmax, nchunk);
+        return hipGetLastError();
+    }
     const int scratch = (int)((1280 + (size_t)rmax * 2 * rmax + 15) & ~(size_t)15);
     const size_t fixed = 768 + (((size_t)m * k + 15) & ~(size_t)15);
     int nwv = 4;

@@ -58,6 +58,18 @@ __device__ __forceinline__ void stream_wait_dyn(int n) {
     }
 }
 
+// 16 bytes per lane from buffer rs at voff into LDS at lds + 16 * lane (nt); offsets past
+// the buffer's range load zeros.  (Device only: in a lambda the builtin would void the
+// kernel's host stub.)
+__device__ __forceinline__ void stream_dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds,
+                                             uint32_t voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, QS_LPTR(lds), 16, voff, 0, 0, 2);
+#else
+    (void)rs, (void)lds, (void)voff;
+#endif
+}
+
 // Byte i of a 4-byte-aligned kernel-argument array through s_load_dword: a byte load
 // (global_load_ubyte, or flat_load after an integer-to-pointer cast) would be a VMEM
 // instruction outside the vmcnt bookkeeping, and its use would drain the ring.
@@ -91,7 +103,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
     int k, int m, int rmax, long long coef_gstride, long long out_gstride, int R, int s_rt,
     int nchunk) {
-    static_assert(KC == 0 || (!DECODE && RC >= 2 && RC <= 6 && S > 0),
+    static_assert(KC == 0 || (!DECODE && RC >= 2 && RC <= 20 && S > 0),
                   "compile-time codes: encode, m <= 6, fixed block size");
     static_assert(S <= 256, "one column word of each sub-row per lane");
     const int s = S ? S : s_rt;                     // sub-row bytes
@@ -123,28 +135,42 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     // ---- issue side (wave-uniform): next piece iss_p of the stream, into slot iss_slot
     int iss_p = 0, iss_slot = 0;
     int issued = 0;                                    // pieces issued
-    const int total = (int)cnt * NP;
     int vm = 0;                                        // VMEM instructions issued
     uint32_t vmv = 0;                                  // lane s: vm index of slot s's last write
     // the 16-byte aligned start of unit u's group, and its last 16-byte chunk (clamp)
+    // A decode unit without output (a group with nothing lost, or a chunk past its losses) is
+    // left out of the stream: its group is not read at all.
+    const long long u_end = g0 + cnt * W;              // past the wave's last unit
+    auto unit_live = [&](long long u) -> bool {
+        if constexpr (!DECODE) return true;
+        const long long g = u / nchunk;
+        return nout[g] - (int)(u - g * nchunk) * RC > 0;
+    };
     long long iss_u = g0;
-    auto unit_src = [&](long long u, int& last) -> const uint8_t* {
+    while (iss_u < u_end && !unit_live(iss_u)) iss_u += W;
+    // The loads go through a buffer resource bounded by the end of the input: the last
+    // 16-byte chunk of a group whose size is 8 mod 16 reaches 8 bytes past it, which past the
+    // last group of the buffer reads as zeros instead of touching unmapped memory.
+    const long long in_bytes = groups * (long long)gb;
+    auto unit_src = [&](long long u, int& last, unsigned& nrec) -> const uint8_t* {
         const long long a = (u / nchunk) * (long long)gb;
         const int sk = (int)(a & 15);
         last = (sk + gb - 1) & ~15;
+        nrec = (unsigned)min(in_bytes - (a - sk), (long long)gb + 32);
         return in + (a - sk);
     };
     int ilast = 0;
-    const uint8_t* isrc = unit_src(g0, ilast);
+    unsigned inrec = 0;
+    const uint8_t* isrc = unit_src(iss_u < u_end ? iss_u : g0, ilast, inrec);
 
     auto issue_one = [&]() {
         const int off = min(iss_p * 1024 + lane * 16, ilast);   // last piece: clamp inside
-        __builtin_amdgcn_global_load_lds(QS_GPTR(isrc + off), QS_LPTR(ring + iss_slot * 1024),
-                                         16, 0, 2);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)isrc, 0, inrec, 0x00020000);
+        stream_dma16(rs, ring + iss_slot * 1024, (uint32_t)off);
         ++vm;
         if (iss_slot < kMirror) {
-            __builtin_amdgcn_global_load_lds(QS_GPTR(isrc + off),
-                                             QS_LPTR(ring + (R + iss_slot) * 1024), 16, 0, 2);
+            stream_dma16(rs, ring + (R + iss_slot) * 1024, (uint32_t)off);
             ++vm;
         }
         vmv = lane == iss_slot ? (uint32_t)(vm - 1) : vmv;
@@ -152,13 +178,15 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
         if (++iss_slot == R) iss_slot = 0;
         if (++iss_p == NP) {
             iss_p = 0;
-            iss_u += W;
-            isrc = unit_src(iss_u, ilast);
+            do {
+                iss_u += W;
+            } while (iss_u < u_end && !unit_live(iss_u));
+            isrc = unit_src(iss_u, ilast, inrec);
         }
     };
     // top the ring up: every piece from `head` on stays, the rest of the R slots refill
     auto fill = [&](int head) {
-        while (issued < total && issued - head < R) issue_one();
+        while (iss_u < u_end && issued - head < R) issue_one();
     };
     // wait until the block at ring position bp has landed (its last piece retired)
     auto wait_block = [&](uint32_t bp) {
@@ -264,7 +292,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     win_build(v.W8, win);
                     static_for<RC>([&](auto jc) __attribute__((always_inline)) {
                         constexpr int j = decltype(jc)::value;
-                        win_apply<cauchy_coef_small(RC, j, decltype(xc)::value)>(acc[j], win);
+                        win_apply<cauchy_coef(RC, j, decltype(xc)::value)>(acc[j], win);
                     });
                     return;
                 }
@@ -341,9 +369,9 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                 }
             }
             asm volatile("" ::: "memory");
+            gbase += NP;                                 // units without output stream nothing
+            gslot0 = (gslot0 + NP) % R;
         }
-        gbase += NP;
-        gslot0 = (gslot0 + NP) % R;
     }
     stream_wait_vmcnt<0>();
 }
@@ -388,7 +416,8 @@ struct RingShape {
     }
 };
 
-template <int K, int S, int RC, bool DECODE, int MC>
+// NT: the encode's parity stores are non-temporal (ring_nt option; decode stores plain)
+template <int K, int S, int RC, bool DECODE, int MC, bool NT = true>
 __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
@@ -398,7 +427,7 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
     constexpr int GB = K * BB, NP = (GB + 1023) / 1024;
     constexpr int NST = RC * 8 * SH::SPR;                 // stores per group, fixed
     constexpr int RCP = RC < 4 ? 4 : RC, NCW = RCP / 4;
-    constexpr int SAUX = DECODE ? 0 : 2;                  // encode's parity stream: nt
+    constexpr int SAUX = (DECODE || !NT) ? 0 : 2;         // encode's parity stream: nt
     constexpr int FM1 = SH::pf(K - 1) + R - 1 - NP;       // next-group pieces issued early
     static_assert(!DECODE || MC == 0, "decode coefficients are per group");
     static_assert(DECODE || MC == RC, "encode: one output per register set");
@@ -658,12 +687,20 @@ int gf_stream_min_ring(int bb) {
     return (max_o + 2 * bb + 1023) / 1024;
 }
 
+// Codes whose encode is compiled (cauchy_const.h coefficients, windowed form) at 1352-byte
+// blocks: BASELINE B/C's (32, 4) and the QuicR presets (quic_fec_group.cc:22-82).
+bool gf_stream_compiled(int k, int m, int bb) {
+    if (bb != 8 * 169) return false;
+    return (k == 32 && m == 4) || (k == 5 && m == 5) || (k == 10 && (m == 10 || m == 15 || m == 20)) ||
+           (k == 15 && m == 15) || (k == 250 && m == 5);
+}
+
 bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& t) {
     (void)m;
     (void)decode;
     if (!t.stream) return false;
     if (bb % 8 != 0 || bb < 8 || bb > 2048) return false;   // s <= 256: a word per lane
-    if (rc != 2 && rc != 4 && rc != 8) return false;
+    if (rc != 2 && rc != 4 && rc != 8 && rc != 16) return false;
     if ((long long)k * bb < 16) return false;   // groups 8 mod 16 apart stream skewed
     if (t.stream_ring < gf_stream_min_ring(bb)) return false;   // gf_apply instead
     return true;
@@ -684,14 +721,16 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     const int per_cu = (int)((160 * 1024) / lds);
     // units: (group, chunk of rc outputs); encode chunks of 8 for m > 8 (m <= 8: one chunk
     // of exactly m outputs), decode chunks of rc for rmax > rc
-    const int nchunk = decode ? (rmax + rc - 1) / rc : (m <= 8 ? 1 : (m + 7) / 8);
+    const int s = bb / 8;
+    const bool compiled = !decode && t.const_enc && gf_stream_compiled(k, m, bb);
+    const int nchunk = decode ? (rmax + rc - 1) / rc
+                              : (compiled || m <= 8 || (rc == 16 && m <= 16)) ? 1 : (m + 7) / 8;
     const long long units = groups * nchunk;
     const long long want = (units + kStreamWaves - 1) / kStreamWaves;
     long long cap = (long long)t.cus * per_cu;
     if (t.stream_grid > 0) cap = t.stream_grid;          // tests: many groups per wave
     const unsigned grid = (unsigned)std::min<long long>(want, cap);
     const unsigned threads = kStreamWaves * 64;
-    const int s = bb / 8;
     // the wave's 32-bit piece counters: cnt * NP, and (gf_ring) cnt groups
     {
         const long long waves = (long long)grid * kStreamWaves;
@@ -707,6 +746,7 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         case 2: QS_GO(2, SV, true, 4, 0); break;          \
         case 4: QS_GO(4, SV, true, 4, 0); break;          \
         case 8: QS_GO(8, SV, true, 8, 0); break;          \
+        case 16: QS_GO(16, SV, true, 16, 0); break;       \
         default: return hipErrorInvalidValue;             \
     }
     // encode: one output per register set, RC = m; the table row stride is max(4, rc)
@@ -734,12 +774,13 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         if ((groups + (long long)rgrid * kRingWaves - 1) / ((long long)rgrid * kRingWaves) >=
             (1LL << 31))
             return hipErrorInvalidValue;
-#define QR_GO(RCV, DEC, MCV)                                                                   \
-    qlaunch((gf_ring_kernel<32, 169, RCV, DEC, MCV>), dim3(rgrid),                   \
+#define QR_GO(RCV, DEC, MCV, NTV)                                                              \
+    qlaunch((gf_ring_kernel<32, 169, RCV, DEC, MCV, NTV>), dim3(rgrid),              \
                        dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax, \
                        coef_gstride, out_gstride)
         note_kernel("gf_ring_kernel<encode,k32m4>");
-        QR_GO(4, false, 4);
+        if (t.ring_nt) QR_GO(4, false, 4, true);
+        else QR_GO(4, false, 4, false);
 #undef QR_GO
         return hipGetLastError();
     }
@@ -752,13 +793,35 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
             QS_DEC(0)
         }
     } else {
-        if ((rc < 4 ? 4 : rc) != (m <= 4 ? 4 : 8)) return hipErrorInvalidValue;
-        if (m > 8 && rc != 8) return hipErrorInvalidValue;
-        if (s == 169 && t.const_enc && k == 32 && m == 4) {
-            // BASELINE configs B/C: the code is fixed at compile time
-            note_kernel("gf_stream_kernel<encode,k32m4>");
-            QS_GO(4, 169, false, 4, 32);
-        } else if (s == 169) {
+        if (compiled) {
+            // BASELINE configs B/C and the QuicR presets at 1350-byte payloads: the code is
+            // fixed at compile time (windowed form, every output in one unit)
+            note_kernel("gf_stream_kernel<encode,compiled>");
+            switch (k * 256 + m) {
+                case 32 * 256 + 4: QS_GO(4, 169, false, 4, 32); break;
+                case 5 * 256 + 5: QS_GO(5, 169, false, 8, 5); break;
+                case 10 * 256 + 10: QS_GO(10, 169, false, 12, 10); break;
+                case 10 * 256 + 15: QS_GO(15, 169, false, 16, 10); break;
+                case 10 * 256 + 20: QS_GO(20, 169, false, 20, 10); break;
+                case 15 * 256 + 15: QS_GO(15, 169, false, 16, 15); break;
+                case 250 * 256 + 5: QS_GO(5, 169, false, 8, 250); break;
+                default: return hipErrorInvalidValue;
+            }
+            return hipGetLastError();
+        }
+        if (m > 8) {
+            // one unit of up to 16 outputs (table rows of 16), or chunks of 8
+            if (rc == 16 && m <= 16) {
+                note_kernel(s == 169 ? "gf_stream_kernel<encode>" : "gf_stream_kernel<encode,s>");
+                if (s == 169) QS_GO(16, 169, false, 16, 0);
+                else QS_GO(16, 0, false, 16, 0);
+                return hipGetLastError();
+            }
+            if (rc != 8) return hipErrorInvalidValue;
+        } else if ((rc < 4 ? 4 : rc) != (m <= 4 ? 4 : 8)) {
+            return hipErrorInvalidValue;
+        }
+        if (s == 169) {
             note_kernel("gf_stream_kernel<encode>");
             QS_ENC(169)
         } else {

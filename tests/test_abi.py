@@ -105,3 +105,47 @@ def test_timing_events_hook_arguments():
     assert L.qfec_set_timing_events(ctypes.c_void_p(1), None) == -2
     assert L.qfec_set_timing_events(None, ctypes.c_void_p(1)) == -2
     assert L.qfec_set_timing_events(None, None) == 0
+
+
+def test_every_host_kernel_stub_has_device_code():
+    """Each kernel a host object registers has a device entry (its .kd descriptor) in the
+    same object's gfx950 code object.  A host pass and a device pass of one source that see
+    different file contents (an edit during a build) leave a stub the runtime cannot
+    resolve: `Cannot find Symbol` and an abort at the first launch."""
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    llvm = "/opt/rocm/lib/llvm/bin"
+    objs = sorted(glob.glob(os.path.join(ROOT, "build", "*.o")))
+    if not objs or not os.path.exists(os.path.join(llvm, "llvm-readelf")):
+        pytest.skip("no build objects or no ROCm llvm tools")
+    tmp = tempfile.mkdtemp()
+    try:
+        checked = nhandles = 0
+        for o in objs:
+            fat = os.path.join(tmp, "fat.bin")
+            r = subprocess.run([os.path.join(llvm, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}",
+                                o, os.path.join(tmp, "scratch.o")], capture_output=True)
+            if r.returncode != 0 or not os.path.exists(fat):
+                continue                                  # host-only object
+            co = os.path.join(tmp, "dev.co")
+            subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", "--type=o",
+                            f"--input={fat}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                            f"--output={co}"], check=True, capture_output=True)
+            dev = subprocess.run([os.path.join(llvm, "llvm-readelf"), "-s", co], check=True,
+                                 capture_output=True, text=True).stdout
+            kd = {ln.split()[-1][:-3] for ln in dev.splitlines() if ln.strip().endswith(".kd")}
+            host = subprocess.run([os.path.join(llvm, "llvm-readelf"), "-s", "-W", o], check=True,
+                                  capture_output=True, text=True).stdout
+            # a kernel's host handle is an 8-byte OBJECT named exactly like the device entry
+            stubs = {ln.split()[-1] for ln in host.splitlines()
+                     if " OBJECT " in ln and " UND " not in ln and "_kernel" in ln.split()[-1]}
+            missing = sorted(stubs - kd)
+            assert not missing, f"{os.path.basename(o)}: host stubs without device code: {missing}"
+            os.remove(fat)
+            checked += 1
+            nhandles += len(stubs)
+        assert checked >= 5 and nhandles >= 100
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
