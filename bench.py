@@ -270,20 +270,26 @@ def pmc_traffic(workload, phase, groups):
 
 
 def packet_protection(eng, k, m, bb, data, parity, steps, stream):
-    """The step next to the codec: SerializeFec's encode + seal of the
-    G*m FEC packets (qfec_encode_seal_batch: header || NullEncrypter tag || parity), the seal
-    alone (qfec_null_seal_batch over the same headers and parity), and the receiver's
-    NullDecrypter open of those packets.  Each call is timed from its kernels with the
-    library's timing events (qfec_set_timing_events).  Reported beside the bench line,
-    never `value`."""
+    """The step next to the codec, each call timed from its kernels
+    with the library's timing events (qfec_set_timing_events):
+      encode_seal  SerializeFec: encode + seal of the G*m FEC packets (qfec_encode_seal_batch)
+      seal         the same G*m seals alone (qfec_null_seal_batch)
+      open         the receiver's NullDecrypter open of those packets (qfec_null_open_batch)
+      seal_groups  every packet of every group, data and FEC, G*(k+m) seals in one launch
+                   (qfec_seal_groups_batch; the reference seals data packets too)
+      open_decode  the receiver batch over those G*(k+m) packets with one data packet per
+                   group lost: open, place, fill the hole, decode (qfec_open_decode_batch)
+    Reported beside the bench line, never `value`."""
     import torch
     from quic_amd import _lib
     lib = _lib.load()
     G = data.shape[0]
     n, hl = G * m, 16
+    per = k + m
+    na = G * per
     stride = (hl + 12 + bb + 3) // 4 * 4
     dev = data.device
-    hdr = torch.arange(n * hl, dtype=torch.int32, device=dev).to(torch.uint8).view(n, hl)
+    hdr = torch.arange(na * hl, dtype=torch.int32, device=dev).to(torch.uint8).view(na, hl)
     pkt = torch.empty((n, stride), dtype=torch.uint8, device=dev)
     pkt2 = torch.empty_like(pkt)
     pkt_len = torch.empty(n, dtype=torch.int32, device=dev)
@@ -291,28 +297,49 @@ def packet_protection(eng, k, m, bb, data, parity, steps, stream):
     # the reference's decrypter copies the whole ciphertext to its output first
     plain = torch.empty((n, (bb + 12 + 3) // 4 * 4), dtype=torch.uint8, device=dev)
     plen = torch.empty(n, dtype=torch.int32, device=dev)
-    ev = DeviceEvents(6)
-    t = {"encode_seal": 0.0, "seal": 0.0, "open": 0.0}
+    apkt = torch.empty((na, stride), dtype=torch.uint8, device=dev)
+    apkt_len = torch.empty(na, dtype=torch.int32, device=dev)
+    g_lost = torch.arange(G, device=dev) * per + (torch.arange(G, device=dev) % k)
+    blocks = torch.empty((G, k, bb), dtype=torch.uint8, device=dev)
+    rows = torch.empty((G, k), dtype=torch.uint8, device=dev)
+    olen = torch.empty(na, dtype=torch.int32, device=dev)
+    rmax = min(k, m)
+    rec = torch.empty((G, rmax, bb), dtype=torch.uint8, device=dev)
+    rec_rows = torch.empty((G, rmax), dtype=torch.uint8, device=dev)
+    status = torch.empty(G, dtype=torch.int32, device=dev)
+    names = ["encode_seal", "seal", "open", "seal_groups", "open_decode"]
+    ev = DeviceEvents(2 * len(names))
+    t = {x: 0.0 for x in names}
     try:
         for i in range(steps + 1):
             lib.qfec_set_timing_events(ev.ev[0], ev.ev[1])
-            eng.encode_seal(k, m, bb, data, parity, hdr, hl, pkt, pkt_len)
+            eng.encode_seal(k, m, bb, data, parity, hdr[:n], hl, pkt, pkt_len)
             lib.qfec_set_timing_events(ev.ev[2], ev.ev[3])
-            eng.null_seal(hdr, hl, parity.view(n, bb), bb, pkt2, pkt_len2)
+            eng.null_seal(hdr[:n], hl, parity.view(n, bb), bb, pkt2, pkt_len2)
             lib.qfec_set_timing_events(ev.ev[4], ev.ev[5])
             eng.null_open(pkt, pkt_len, hl, plain, plen)
+            lib.qfec_set_timing_events(ev.ev[6], ev.ev[7])
+            eng.seal_groups(k, m, bb, data, parity, hdr, hl, bb, apkt, apkt_len)
+            lib.qfec_set_timing_events(None, None)
+            apkt_len[g_lost] = -1
+            lib.qfec_set_timing_events(ev.ev[8], ev.ev[9])
+            eng.open_decode(k, m, bb, apkt, apkt_len, hl, blocks, rows, olen, rec, rec_rows,
+                            status)
             lib.qfec_set_timing_events(None, None)
             torch.cuda.synchronize(dev)
             if i:   # the first pass is warmup
-                t["encode_seal"] += ev.elapsed_ms(0, 1) / steps
-                t["seal"] += ev.elapsed_ms(2, 3) / steps
-                t["open"] += ev.elapsed_ms(4, 5) / steps
+                for q, x in enumerate(names):
+                    t[x] += ev.elapsed_ms(2 * q, 2 * q + 1) / steps
     finally:
         lib.qfec_set_timing_events(None, None)
         ev.close()
+    lost_i = torch.arange(G, device=dev) % k
     ok = (bool((plen == bb).all()) and torch.equal(plain[:, :bb], parity.view(n, bb))
-          and torch.equal(pkt, pkt2))
+          and torch.equal(pkt, pkt2) and bool((status == 0).all())
+          and bool((rec_rows[:, 0] == lost_i.to(torch.uint8)).all())
+          and torch.equal(rec[:, 0], data[torch.arange(G, device=dev), lost_i]))
     pkt_bytes = n * (hl + 12 + bb)
+    all_bytes = na * (hl + 12 + bb)
     return {"packets": n, "header_bytes": hl, "encrypter": "NullEncrypter (FNV-1a-128 tag)",
             "encode_seal_ms": round(t["encode_seal"], 5), "seal_ms": round(t["seal"], 5),
             "open_ms": round(t["open"], 5),
@@ -320,9 +347,15 @@ def packet_protection(eng, k, m, bb, data, parity, steps, stream):
             "open_Mpkt_s": round(n / t["open"] / 1e3, 2),
             "seal_GBps": round(pkt_bytes / t["seal"] / 1e6, 1),
             "open_GBps": round(pkt_bytes / t["open"] / 1e6, 1),
+            "group_packets": na,
+            "seal_groups_ms": round(t["seal_groups"], 5),
+            "seal_groups_GBps": round(all_bytes / t["seal_groups"] / 1e6, 1),
+            "open_decode_ms": round(t["open_decode"], 5),
+            "open_decode_GBps": round(all_bytes / t["open_decode"] / 1e6, 1),
             "round_trip_ok": ok,
             "note": "kernel-bracketing events per call; one lane per packet (serial FNV "
-                    "chain), DESIGN.md 6.2"}
+                    "chain, six 22-bit limbs), DESIGN.md 6.2; open_decode loses data "
+                    "packet g % k of group g"}
 
 
 def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps, recovered):

@@ -181,6 +181,47 @@ QFEC_API int qfec_encode_seal_batch(qfec_ctx *ctx, int k, int m, int block_bytes
                                     unsigned char *d_pkt, long long pkt_stride, int *d_pkt_len,
                                     void *stream);
 
+/* Every packet of each group in one launch: the reference seals each data packet
+ * (quic_packet_creator.cc:733-736) as well as each FEC packet (:948-953).  Packet
+ * p = g*(k+m) + i is sealed with header row p (d_hdr + p*hdr_stride, d_hdr_len[p] or
+ * hdr_len_all bytes) as the associated data and, as plaintext, data block (g, i) of d_data
+ * [G][k][bb] for i < k or parity block (g, i-k) of d_parity [G][m][bb] otherwise, its first
+ * d_pt_len[p] (or pt_len_all <= bb) bytes: d_pkt + p*pkt_stride = header || tag12 || PT,
+ * d_pkt_len[p] as in qfec_null_seal_batch.  k + m <= 256. */
+QFEC_API int qfec_seal_groups_batch(qfec_ctx *ctx, int k, int m, int block_bytes,
+                                    long long groups, const unsigned char *d_data,
+                                    const unsigned char *d_parity, const unsigned char *d_hdr,
+                                    long long hdr_stride, const int *d_hdr_len, int hdr_len_all,
+                                    const int *d_pt_len, int pt_len_all, unsigned char *d_pkt,
+                                    long long pkt_stride, int *d_pkt_len, void *stream);
+/* qfec_encode_batch into d_parity, then qfec_seal_groups_batch: one call, two launches. */
+QFEC_API int qfec_encode_seal_groups_batch(qfec_ctx *ctx, int k, int m, int block_bytes,
+                                           long long groups, const unsigned char *d_data,
+                                           unsigned char *d_parity, const unsigned char *d_hdr,
+                                           long long hdr_stride, const int *d_hdr_len,
+                                           int hdr_len_all, const int *d_pt_len, int pt_len_all,
+                                           unsigned char *d_pkt, long long pkt_stride,
+                                           int *d_pkt_len, void *stream);
+/* Receiver side: NullDecrypter::DecryptPacket on every packet of each group (the framer
+ * decrypts before the group sees a packet, quic_framer.cc:657), then the group decode.
+ * Wire packet p = g*(k+m) + i at d_pkt + p*pkt_stride, d_pkt_len[p] bytes (< 0: not
+ * received), the first d_ad_len[p] (or ad_len_all) of them the associated data.
+ *   d_open_len [G][k+m]  plaintext bytes of packet p, or -1 (not received, malformed,
+ *                        plaintext longer than bb, or tag mismatch)
+ *   d_blocks [G][k][bb]  data packet i's plaintext, zero-padded, in slot i; each slot whose
+ *                        data packet did not open holds the plaintext of the next opened FEC
+ *                        packet (ascending)
+ *   d_rows [G][k]        the row tag of each slot (i, or k + j for FEC packet j; 255 when no
+ *                        opened FEC packet is left, and the group's status is then -3)
+ * followed by qfec_decode_batch_recovered(d_blocks, d_rows) into d_rec / d_rec_rows /
+ * d_status.  Three launches on one stream.  k + m <= 255. */
+QFEC_API int qfec_open_decode_batch(qfec_ctx *ctx, int k, int m, int block_bytes,
+                                    long long groups, const unsigned char *d_pkt,
+                                    long long pkt_stride, const int *d_pkt_len,
+                                    const int *d_ad_len, int ad_len_all, unsigned char *d_blocks,
+                                    unsigned char *d_rows, int *d_open_len, unsigned char *d_rec,
+                                    unsigned char *d_rec_rows, int *d_status, void *stream);
+
 /* ---------------------------------------------------------------------------------
  * Support: the coefficient tables, a seeded synthetic workload, diagnostics.
  * ------------------------------------------------------------------------------- */

@@ -20,6 +20,7 @@
 #include "../../include/quic_fec.h"
 #include "fec_kernels.h"
 #include "gf256.h"
+#include "pp_null.h"
 
 // ------------------------------------------------------------- Cauchy table blob
 // quic_amd/data/cauchy_256_tables.bin (tools/gen_cauchy_tables.py) embedded at build time:
@@ -151,6 +152,7 @@ struct qfec_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     qfec::Tune tune;
+    int pp_hash = 0;   // packet protection's FNV chain: 0 six 22-bit limbs, 1 64-bit halves
     // The decode workspace (dcoef, dslots, dnout, dscratch) is one per context.  Calls may
     // enqueue on any stream: a use on another stream than the previous use records ws_ev on
     // that previous stream and waits for it, so uses of the workspace are ordered across
@@ -619,6 +621,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
+        {"pp_hash", &c->pp_hash, 0, 1},
     };
     for (const Opt& o : opts) {
         if (strcmp(o.n, name) != 0) continue;
@@ -643,7 +646,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol}, {"dcol_cache", t.dcol_cache}, {"stream_rc16", t.stream_rc16},
         {"ring_nt", t.ring_nt},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
-        {"host_chunk_mb", t.host_chunk_mb},
+        {"host_chunk_mb", t.host_chunk_mb}, {"pp_hash", c->pp_hash},
     };
     for (const auto& o : opts)
         if (strcmp(o.first, name) == 0) { *value = o.second; return 0; }
@@ -740,7 +743,7 @@ int qfec_null_seal_batch(qfec_ctx* c, long long n, const unsigned char* d_ad, lo
     std::lock_guard<std::mutex> lk(c->mu);
     int rc;
     if ((rc = set_device(c))) return rc;
-    QF_HIP(qfec::launch_null_seal(n, d_ad, ad_stride, (const int32_t*)d_ad_len, ad_len_all, d_pt,
+    QF_HIP(qfec::launch_null_seal_h(c->pp_hash, n, d_ad, ad_stride, (const int32_t*)d_ad_len, ad_len_all, d_pt,
                                   pt_stride, (const int32_t*)d_pt_len, pt_len_all, d_out,
                                   out_stride, (int32_t*)d_out_len, pick(c, stream)));
     return 0;
@@ -757,7 +760,7 @@ int qfec_null_open_batch(qfec_ctx* c, long long n, const unsigned char* d_pkt, l
     std::lock_guard<std::mutex> lk(c->mu);
     int rc;
     if ((rc = set_device(c))) return rc;
-    QF_HIP(qfec::launch_null_open(n, d_pkt, pkt_stride, (const int32_t*)d_pkt_len, pkt_len_all,
+    QF_HIP(qfec::launch_null_open_h(c->pp_hash, n, d_pkt, pkt_stride, (const int32_t*)d_pkt_len, pkt_len_all,
                                   (const int32_t*)d_ad_len, ad_len_all, d_out, out_stride,
                                   (int32_t*)d_out_len, pick(c, stream)));
     return 0;
@@ -780,10 +783,89 @@ int qfec_encode_seal_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
     // SerializeFec (quic_packet_creator.cc:935-957): parity packets from the group's encode,
     // each sealed with its packet header as the associated data; packet (g, i) = g * m + i
     if ((rc = encode_impl(c, k, m, bb, groups, d_data, d_parity, st))) return rc;
-    QF_HIP(qfec::launch_null_seal(groups * m, d_hdr, hdr_stride, (const int32_t*)d_hdr_len,
+    QF_HIP(qfec::launch_null_seal_h(c->pp_hash, groups * m, d_hdr, hdr_stride, (const int32_t*)d_hdr_len,
                                   hdr_len_all, d_parity, bb, nullptr, bb, d_pkt, pkt_stride,
                                   (int32_t*)d_pkt_len, st));
     return 0;
+}
+
+// Every packet of each group, data and FEC, in one launch (quic_packet_creator.cc:733-736
+// seals each data packet, :948-953 each FEC packet); packet (g, i) = g * (k + m) + i.
+static int seal_groups_args(qfec_ctx* c, int k, int m, int bb, long long groups,
+                            const unsigned char* d_data, const unsigned char* d_parity,
+                            const unsigned char* d_hdr, long long hdr_stride, const int* d_hdr_len,
+                            int hdr_len_all, const int* d_pt_len, int pt_len_all,
+                            const unsigned char* d_pkt, long long pkt_stride, const int* d_pkt_len) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    if (k + m > 256) return fail(-2, "k + m > 256");
+    if (groups && (!d_data || !d_parity || !d_pkt || !d_pkt_len || (!d_hdr && (d_hdr_len || hdr_len_all))))
+        return fail(-2, "null buffer");
+    if (hdr_stride < 0 || pkt_stride < 0) return fail(-2, "bad stride");
+    if (!d_pt_len && (pt_len_all < 0 || pt_len_all > bb)) return fail(-2, "pt_len_all outside 0..block_bytes");
+    if ((((uintptr_t)d_pkt) | (uintptr_t)pkt_stride) & 3) return fail(-2, "pkt / pkt_stride not 4-byte aligned");
+    return 0;
+}
+
+int qfec_seal_groups_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
+                           const unsigned char* d_data, const unsigned char* d_parity,
+                           const unsigned char* d_hdr, long long hdr_stride, const int* d_hdr_len,
+                           int hdr_len_all, const int* d_pt_len, int pt_len_all,
+                           unsigned char* d_pkt, long long pkt_stride, int* d_pkt_len, void* stream) {
+    int rc = seal_groups_args(c, k, m, bb, groups, d_data, d_parity, d_hdr, hdr_stride, d_hdr_len,
+                              hdr_len_all, d_pt_len, pt_len_all, d_pkt, pkt_stride, d_pkt_len);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    QF_HIP(qfec::launch_null_seal_groups(c->pp_hash, k, m, bb, groups, d_data, d_parity, d_hdr, hdr_stride,
+                                         (const int32_t*)d_hdr_len, hdr_len_all,
+                                         (const int32_t*)d_pt_len, pt_len_all, d_pkt, pkt_stride,
+                                         (int32_t*)d_pkt_len, pick(c, stream)));
+    return 0;
+}
+
+int qfec_encode_seal_groups_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
+                                  const unsigned char* d_data, unsigned char* d_parity,
+                                  const unsigned char* d_hdr, long long hdr_stride,
+                                  const int* d_hdr_len, int hdr_len_all, const int* d_pt_len,
+                                  int pt_len_all, unsigned char* d_pkt, long long pkt_stride,
+                                  int* d_pkt_len, void* stream) {
+    int rc = seal_groups_args(c, k, m, bb, groups, d_data, d_parity, d_hdr, hdr_stride, d_hdr_len,
+                              hdr_len_all, d_pt_len, pt_len_all, d_pkt, pkt_stride, d_pkt_len);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    const hipStream_t st = pick(c, stream);
+    if ((rc = encode_impl(c, k, m, bb, groups, d_data, d_parity, st))) return rc;
+    QF_HIP(qfec::launch_null_seal_groups(c->pp_hash, k, m, bb, groups, d_data, d_parity, d_hdr, hdr_stride,
+                                         (const int32_t*)d_hdr_len, hdr_len_all,
+                                         (const int32_t*)d_pt_len, pt_len_all, d_pkt, pkt_stride,
+                                         (int32_t*)d_pkt_len, st));
+    return 0;
+}
+
+// Receiver: open every packet of each group (quic_framer.cc:657 decrypts before the group
+// sees a packet), place the data plaintexts, fill the holes with opened FEC packets, decode.
+int qfec_open_decode_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
+                           const unsigned char* d_pkt, long long pkt_stride, const int* d_pkt_len,
+                           const int* d_ad_len, int ad_len_all, unsigned char* d_blocks,
+                           unsigned char* d_rows, int* d_open_len, unsigned char* d_rec,
+                           unsigned char* d_rec_rows, int* d_status, void* stream) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    if (k + m > 255) return fail(-2, "k + m > 255 (row tag 255 marks an unfilled slot)");
+    if (groups && (!d_pkt || !d_pkt_len || !d_blocks || !d_rows || !d_open_len || !d_rec || !d_rec_rows))
+        return fail(-2, "null buffer");
+    if (pkt_stride <= 0 && groups) return fail(-2, "bad pkt_stride");
+    if (!d_ad_len && ad_len_all < 0) return fail(-2, "bad ad_len_all");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    const hipStream_t st = pick(c, stream);
+    QF_HIP(qfec::launch_open_groups(c->pp_hash, k, m, bb, groups, d_pkt, pkt_stride, (const int32_t*)d_pkt_len,
+                                    (const int32_t*)d_ad_len, ad_len_all, d_blocks, d_rows,
+                                    (int32_t*)d_open_len, st));
+    return decode_recovered_impl(c, k, m, bb, groups, d_blocks, d_rows, d_rec, d_rec_rows,
+                                 (int32_t*)d_status, st);
 }
 
 int qfec_decode_batch_recovered_host(qfec_ctx* c, int k, int m, int bb, long long groups,

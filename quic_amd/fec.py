@@ -224,6 +224,37 @@ class FecEngine:
         if rc:
             raise FecError(rc, "qfec_encode_seal_batch")
 
+    def seal_groups(self, k, m, block_bytes, data, parity, hdr, hdr_len, pt_len, pkt, pkt_len,
+                    encode=False, stream=None):
+        """Seal every packet of each group in one launch: packet p = g*(k+m)+i =
+        hdr[p][:hdr_len] || tag12 || (data[g][i] if i < k else parity[g][i-k])[:pt_len] into
+        pkt [G*(k+m)][pkt_stride]; pkt_len int32 [G*(k+m)].  encode=True first encodes data
+        into parity (qfec_encode_seal_groups_batch)."""
+        G = data.shape[0]
+        h, h_all = self._lens(hdr_len)
+        p, p_all = self._lens(pt_len)
+        fn = self.lib.qfec_encode_seal_groups_batch if encode else self.lib.qfec_seal_groups_batch
+        rc = fn(self._h, k, m, block_bytes, G, _dptr(data), _dptr(parity), _dptr(hdr),
+                hdr.stride(0), h, h_all, p, p_all, _dptr(pkt), pkt.stride(0), _dptr(pkt_len),
+                _stream(stream, data))
+        if rc:
+            raise FecError(rc, "qfec_encode_seal_groups_batch" if encode else "qfec_seal_groups_batch")
+
+    def open_decode(self, k, m, block_bytes, pkt, pkt_len, ad_len, blocks, rows, open_len, rec,
+                    rec_rows, status=None, stream=None):
+        """Receiver: open every wire packet pkt [G*(k+m)][stride] (pkt_len int32, < 0 = not
+        received), place the plaintexts into blocks [G][k][bb] / rows [G][k], then the
+        recovered-layout decode into rec / rec_rows / status.  open_len int32 [G*(k+m)]."""
+        G = blocks.shape[0]
+        a, a_all = self._lens(ad_len)
+        rc = self.lib.qfec_open_decode_batch(self._h, k, m, block_bytes, G, _dptr(pkt),
+                                             pkt.stride(0), _dptr(pkt_len), a, a_all,
+                                             _dptr(blocks), _dptr(rows), _dptr(open_len),
+                                             _dptr(rec), _dptr(rec_rows), _dptr(status),
+                                             _stream(stream, pkt))
+        if rc:
+            raise FecError(rc, "qfec_open_decode_batch")
+
     # host-pointer batch calls (synchronous; include H2D/D2H)
     def encode_host(self, k, m, block_bytes, data):
         data = np.ascontiguousarray(data, dtype=np.uint8)

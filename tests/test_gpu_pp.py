@@ -22,7 +22,18 @@ def _host(t):
     return t.cpu().numpy()
 
 
-def test_known_answer_through_gpu(engine):
+@pytest.fixture(params=[0, 1], ids=["limbs", "halves"])
+def pp_engine(request, engine):
+    """The engine with either FNV-1a-128 chain (context option pp_hash)."""
+    engine.set_option("pp_hash", request.param)
+    try:
+        yield engine
+    finally:
+        engine.set_option("pp_hash", 0)
+
+
+def test_known_answer_through_gpu(pp_engine):
+    engine = pp_engine
     import torch
     ad = _dev(np.frombuffer(KAT_AD, np.uint8).reshape(1, -1))
     pt = _dev(np.frombuffer(KAT_PT, np.uint8).reshape(1, -1))
@@ -41,8 +52,9 @@ def test_known_answer_through_gpu(engine):
 
 @pytest.mark.parametrize("n,S,AS", [(1, 64, 16), (63, 200, 21), (300, 1352, 19),
                                     (517, 1400, 33), (70, 9008, 16)])
-def test_seal_open_random_vs_oracle(engine, oracle, n, S, AS):
+def test_seal_open_random_vs_oracle(pp_engine, oracle, n, S, AS):
     import torch
+    engine = pp_engine
     rng = np.random.default_rng(n * 7 + S)
     ad = rng.integers(0, 256, (n, AS), dtype=np.uint8)
     pt = rng.integers(0, 256, (n, S), dtype=np.uint8)
@@ -172,3 +184,174 @@ def test_lengths_beyond_row_stride_rejected(engine, oracle):
     engine.null_open(_dev(pkt), _dev(pkt_len), _dev(adl), out_o, len_o)
     assert np.array_equal(_host(len_o), eres_o)
     assert np.array_equal(_host(out_o), exp_o)
+
+
+# ---------------------------------------------------------------- grouped forms
+def _group_packets(oracle, k, m, bb, G, rng, hmax=20):
+    """Data blocks whose payloads are zero-padded to bb, their parity, per-packet headers
+    and plaintext lengths, and the oracle's wire packets for packet p = g*(k+m)+i."""
+    per = k + m
+    n = G * per
+    data = rng.integers(0, 256, (G, k, bb), dtype=np.uint8)
+    pt_len = np.full((G, per), bb, np.int32)
+    pt_len[:, :k] = rng.integers(max(0, bb - 300), bb + 1, (G, k))
+    for g in range(G):
+        for i in range(k):
+            data[g, i, pt_len[g, i]:] = 0          # a data block is its payload, zero-padded
+    parity, rc = oracle.encode_batch(k, m, bb, data)
+    assert rc == 0
+    rows_pt = np.concatenate([data, parity], axis=1).reshape(n, bb)
+    hdr = rng.integers(0, 256, (n, hmax), dtype=np.uint8)
+    hdr_len = rng.integers(9, hmax + 1, n).astype(np.int32)
+    stride = (hmax + 12 + bb + 3) // 4 * 4
+    pkt, plen = oracle.null_seal_batch(hdr, hdr_len, rows_pt, pt_len.reshape(n), stride)
+    assert (plen >= 0).all()
+    return data, parity, pt_len.reshape(n), hdr, hdr_len, pkt, plen
+
+
+@pytest.mark.parametrize("k,m,G,encode", [(10, 1, 37, True), (5, 5, 21, False),
+                                          (32, 4, 9, True), (10, 20, 6, False)])
+def test_seal_groups_vs_oracle(pp_engine, oracle, k, m, G, encode):
+    """Every data and FEC packet of each group in one launch, bit-exact with the oracle's
+    per-packet NullEncrypter (quic_packet_creator.cc:733-736, :948-953)."""
+    import torch
+    engine = pp_engine
+    bb = 1352
+    rng = np.random.default_rng(k * 1000 + m * 10 + G)
+    data, parity, pt_len, hdr, hdr_len, exp, eres = _group_packets(oracle, k, m, bb, G, rng)
+    n = G * (k + m)
+    d_par = torch.zeros((G, m, bb), dtype=torch.uint8, device="cuda") if encode else _dev(parity)
+    pkt = torch.zeros((n, exp.shape[1]), dtype=torch.uint8, device="cuda")
+    pkt_len = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    engine.seal_groups(k, m, bb, _dev(data), d_par, _dev(hdr), _dev(hdr_len), _dev(pt_len),
+                       pkt, pkt_len, encode=encode)
+    assert np.array_equal(_host(d_par), parity)
+    assert np.array_equal(_host(pkt_len), eres)
+    assert np.array_equal(_host(pkt), exp)
+
+
+def _expected_open_decode(oracle, k, m, bb, G, pkt, pkt_len, hdr_len):
+    """open_len, blocks, rows as qfec_open_decode_batch documents them, from the oracle's
+    NullDecrypter; then the oracle decode of the groups that have k opened packets."""
+    from tests.test_gpu_parity import expected_recovered
+    per = k + m
+    n = G * per
+    o_stride = (bb + 12 + 3) // 4 * 4 + 64
+    rcv = pkt_len >= 0
+    plain, res = oracle.null_open_batch(pkt, np.where(rcv, pkt_len, hdr_len), hdr_len, o_stride)
+    open_len = np.where(rcv & (res <= bb), res, -1).astype(np.int32)
+    blocks = np.zeros((G, k, bb), np.uint8)
+    rows = np.full((G, k), 255, np.uint8)
+    for g in range(G):
+        ol = open_len[g * per:(g + 1) * per]
+        avail = [j for j in range(m) if ol[k + j] >= 0]
+        h = 0
+        for i in range(k):
+            p = g * per + i
+            if ol[i] >= 0:
+                rows[g, i] = i
+                blocks[g, i, :ol[i]] = plain[p, :ol[i]]
+            elif h < len(avail):
+                j = avail[h]
+                h += 1
+                rows[g, i] = k + j
+                q = g * per + k + j
+                blocks[g, i, :ol[k + j]] = plain[q, :ol[k + j]]
+    ok = (rows != 255).all(axis=1)
+    rec = np.zeros((G, min(k, m), bb), np.uint8)
+    rec_rows = np.full((G, min(k, m)), 255, np.uint8)
+    status = np.full(G, -3, np.int32)
+    if ok.any():
+        b_or, r_or, s_or = oracle.decode_batch(k, m, bb, blocks[ok], rows[ok])
+        r_ok, rr_ok = expected_recovered(k, m, bb, rows[ok], b_or, r_or, s_or)
+        rec[ok], rec_rows[ok], status[ok] = r_ok, rr_ok, s_or
+    return open_len, blocks, rows, ok, rec, rec_rows, status
+
+
+@pytest.mark.parametrize("k,m,G,bb", [(10, 1, 40, 1352), (5, 5, 30, 1352), (32, 4, 12, 1352),
+                                      (10, 20, 9, 1352), (8, 1, 16, 1350)])
+def test_open_decode_vs_oracle(pp_engine, oracle, k, m, G, bb):
+    """Receiver batch: open (NullDecrypter) every packet of each group, place the data
+    plaintexts, fill the holes with opened FEC packets, decode -- against the oracle's open
+    and decode.  Lost packets, tampered packets (rejected by the tag) and one group that
+    cannot be recovered."""
+    import torch
+    engine = pp_engine
+    rng = np.random.default_rng(k * 77 + m + G)
+    per, n = k + m, G * (k + m)
+    data, parity, pt_len, hdr, hdr_len, pkt, plen = _group_packets(oracle, k, m, bb, G, rng)
+    pkt_len = plen.copy()
+    q = 0.4 * m / per                                   # about 0.4 m erasures per group
+    lost = rng.random(n) < 0.7 * q
+    pkt_len[lost] = -1
+    bad = np.flatnonzero(~lost & (rng.random(n) < 0.3 * q))
+    bad = bad if len(bad) else np.array([n - 1])
+    for p in bad:
+        pkt[p, hdr_len[p] + int(rng.integers(0, 12 + pt_len[p]))] ^= 1 << int(rng.integers(0, 8))
+    pkt_len[0] = -1                                     # group 0: a data packet lost and
+    pkt_len[k:per] = -1                                 # no FEC packet left to replace it
+    open_len, blocks, rows, ok, rec, rec_rows, status = _expected_open_decode(
+        oracle, k, m, bb, G, pkt, pkt_len, hdr_len)
+    assert not ok[0] and ok.sum() >= G // 3
+    d_blocks = torch.zeros((G, k, bb), dtype=torch.uint8, device="cuda")
+    d_rows = torch.zeros((G, k), dtype=torch.uint8, device="cuda")
+    d_ol = torch.zeros(n, dtype=torch.int32, device="cuda")
+    d_rec = torch.zeros((G, min(k, m), bb), dtype=torch.uint8, device="cuda")
+    d_rr = torch.zeros((G, min(k, m)), dtype=torch.uint8, device="cuda")
+    d_st = torch.full((G,), 99, dtype=torch.int32, device="cuda")
+    engine.open_decode(k, m, bb, _dev(pkt), _dev(pkt_len), _dev(hdr_len), d_blocks, d_rows, d_ol,
+                       d_rec, d_rr, d_st)
+    assert np.array_equal(_host(d_ol), open_len)
+    assert np.array_equal(_host(d_rows), rows)
+    gb = _host(d_blocks)
+    filled = rows != 255
+    assert np.array_equal(gb[filled], blocks[filled])
+    assert np.array_equal(_host(d_st), status)
+    assert np.array_equal(_host(d_rr)[ok], rec_rows[ok])
+    got_rec = _host(d_rec)
+    used = rec_rows != 255
+    assert np.array_equal(got_rec[used], rec[used])
+    # the recovered blocks are the lost data blocks
+    for g in np.flatnonzero(ok):
+        for j in range(min(k, m)):
+            if rec_rows[g, j] != 255:
+                assert np.array_equal(got_rec[g, j], data[g, rec_rows[g, j]])
+
+
+def test_open_decode_full_size_a_shape(engine):
+    """BASELINE config A's shape, 65,536 groups of (10 + 1) x 1352 B: every packet of every
+    group sealed in one launch after the encode, one random packet per group lost, then
+    open -> place -> decode: each group's lost data block comes back (a round trip, no
+    oracle at this size)."""
+    import torch
+    from quic_amd import fec
+    G, k, m, bb, hl = 65536, 10, 1, 1352, 16
+    per, n = k + m, 65536 * 11
+    data = torch.empty((G, k, bb), dtype=torch.uint8, device="cuda")
+    fec.synth_fill(data, seed=5)
+    parity = torch.empty((G, m, bb), dtype=torch.uint8, device="cuda")
+    hdr = torch.arange(n * hl, dtype=torch.int32, device="cuda").to(torch.uint8).view(n, hl)
+    stride = (hl + 12 + bb + 3) // 4 * 4
+    pkt = torch.empty((n, stride), dtype=torch.uint8, device="cuda")
+    pkt_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    engine.seal_groups(k, m, bb, data, parity, hdr, hl, bb, pkt, pkt_len, encode=True)
+    torch.cuda.synchronize()
+    assert bool((pkt_len == hl + 12 + bb).all())
+    lose = torch.randint(0, per, (G,), device="cuda")
+    rcv_len = pkt_len.clone().view(G, per)
+    rcv_len[torch.arange(G, device="cuda"), lose] = -1
+    blocks = torch.empty((G, k, bb), dtype=torch.uint8, device="cuda")
+    rows = torch.empty((G, k), dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    rec = torch.empty((G, 1, bb), dtype=torch.uint8, device="cuda")
+    rr = torch.empty((G, 1), dtype=torch.uint8, device="cuda")
+    st = torch.empty(G, dtype=torch.int32, device="cuda")
+    engine.open_decode(k, m, bb, pkt, rcv_len.view(n), hl, blocks, rows, ol, rec, rr, st)
+    torch.cuda.synchronize()
+    assert bool((st == 0).all())
+    assert bool(((ol.view(G, per) == bb) | (rcv_len < 0)).all())
+    lost_data = lose < k
+    assert bool((rr[:, 0][lost_data] == lose[lost_data].to(torch.uint8)).all())
+    assert bool((rr[:, 0][~lost_data] == 255).all())
+    gi = torch.nonzero(lost_data).flatten()
+    assert torch.equal(rec[gi, 0], data[gi, lose[gi]])
