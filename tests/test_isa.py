@@ -31,7 +31,7 @@ def stream_isa(tmp_path_factory, request):
     built = os.path.join(ROOT, "build", f"{name}-hip-amdgcn-amd-amdhsa-gfx950.s")
     csrc = os.path.join(ROOT, "quic_amd", "csrc")
     inputs = [src] + [os.path.join(csrc, h) for h in ("fec_kernels.h", "gf_bitslice.h", "gf256.h")]
-    inputs += [os.path.join(ROOT, "tools", "gen_cauchy_const.py"), os.path.join(ROOT, "Makefile")]
+    inputs += [os.path.join(ROOT, "tools", "gen_cauchy_const.py")]
     if os.path.exists(built) and all(os.path.getmtime(built) >= os.path.getmtime(f)
                                      for f in inputs):
         out = built
