@@ -1,0 +1,39 @@
+#!/bin/bash
+# One parameterised GPU session: every step this repo runs on the gpurun box, by name.
+#   gpurun --timeout 1200 -- 'bash tools/gpu_steps.sh <step> [<step> ...]'
+# Steps (output in gpurun_out/<label>.log; the session stops at the first fault, abort or
+# time limit, see tools/gpu_session.sh):
+#   tests                 the whole -m gpu suite
+#   tests:<file|-k expr>  one test file (tests/test_gpu_pp.py) or a -k selection
+#   smoke                 __graft_entry__.smoke()
+#   bench:<W>[:<args>]    bench.py --workload W --verify (W = A B C D), extra args after ':'
+#   quick:<W>[:<args>]    bench.py --workload W, no CPU baseline, no host leg, 10 steps
+#   preset:<k>,<m>        quick bench of a QuicR preset
+#   prof:<W>[:<args>]     rocprofv3 --kernel-trace --stats of a quick bench
+#   pmc:<W>[:<args>]      tools/pmc.sh passes (FETCH/WRITE traffic, waves, issue mix)
+# Extra args use ',' for spaces: quick:B:--opt,ring_nt=0.  GPU_STEPS_DRY=1 prints the steps.
+export TMPDIR=/tmp
+specs=()
+for step in "$@"; do
+  kind="${step%%:*}"; rest=""; [ "$step" != "$kind" ] && rest="${step#*:}"
+  W="${rest%%:*}"; extra=""; [ "$rest" != "$W" ] && extra="${rest#*:}"
+  extra="${extra//,/ }"
+  tag=$(echo "$step" | tr -c 'A-Za-z0-9_\n' '_')
+  quick="python bench.py --no-cpu-baseline --no-host --steps 10 --warmup 3"
+  case "$kind" in
+    tests)
+      if [ -z "$rest" ]; then sel="tests"
+      elif [ -f "$rest" ]; then sel="$rest"
+      else sel="tests -k '$rest'"; fi
+      specs+=("$tag::900::python -u -m pytest $sel -m gpu -x -q --timeout 120 --timeout-method thread") ;;
+    smoke)  specs+=("smoke::300::python -c 'import __graft_entry__ as g; g.smoke()'") ;;
+    bench)  specs+=("$tag::600::python bench.py --workload $W --verify $extra") ;;
+    quick)  specs+=("$tag::300::$quick --workload $W $extra") ;;
+    preset) specs+=("$tag::300::$quick --preset $W $extra") ;;
+    prof)   specs+=("$tag::300::rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run --output-format csv -- $quick --workload $W $extra") ;;
+    pmc)    specs+=("$tag::600::bash tools/pmc.sh $W $tag $extra") ;;
+    *) echo "unknown step: $step"; exit 2 ;;
+  esac
+done
+if [ -n "$GPU_STEPS_DRY" ]; then printf '%s\n' "${specs[@]}"; exit 0; fi
+exec tools/gpu_session.sh "${specs[@]}"
