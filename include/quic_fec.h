@@ -214,7 +214,8 @@ QFEC_API int qfec_encode_seal_groups_batch(qfec_ctx *ctx, int k, int m, int bloc
  *   d_rows [G][k]        the row tag of each slot (i, or k + j for FEC packet j; 255 when no
  *                        opened FEC packet is left, and the group's status is then -3)
  * followed by qfec_decode_batch_recovered(d_blocks, d_rows) into d_rec / d_rec_rows /
- * d_status.  Three launches on one stream.  k + m <= 255. */
+ * d_status (a group with an unfilled slot: status -3, recovered rows all 255).  Four
+ * launches on one stream.  k + m <= 255. */
 QFEC_API int qfec_open_decode_batch(qfec_ctx *ctx, int k, int m, int block_bytes,
                                     long long groups, const unsigned char *d_pkt,
                                     long long pkt_stride, const int *d_pkt_len,

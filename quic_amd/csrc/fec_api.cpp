@@ -864,8 +864,12 @@ int qfec_open_decode_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
     QF_HIP(qfec::launch_open_groups(c->pp_hash, k, m, bb, groups, d_pkt, pkt_stride, (const int32_t*)d_pkt_len,
                                     (const int32_t*)d_ad_len, ad_len_all, d_blocks, d_rows,
                                     (int32_t*)d_open_len, st));
-    return decode_recovered_impl(c, k, m, bb, groups, d_blocks, d_rows, d_rec, d_rec_rows,
-                                 (int32_t*)d_status, st);
+    if ((rc = decode_recovered_impl(c, k, m, bb, groups, d_blocks, d_rows, d_rec, d_rec_rows,
+                                    (int32_t*)d_status, st)))
+        return rc;
+    QF_HIP(qfec::launch_open_status(k, std::min(k, m), groups, d_rows, d_rec_rows,
+                                    (int32_t*)d_status, st));
+    return 0;
 }
 
 int qfec_decode_batch_recovered_host(qfec_ctx* c, int k, int m, int bb, long long groups,

@@ -40,4 +40,9 @@ hipError_t launch_open_groups(int form, int k, int m, int bb, long long groups, 
                               const int32_t* ad_len, int ad_all, uint8_t* blocks,
                               uint8_t* rows, int32_t* open_len, hipStream_t st);
 
+// After the decode of an open batch: groups with an unfilled slot get status -3 and no
+// recovered rows.
+hipError_t launch_open_status(int k, int rmax, long long groups, const uint8_t* rows,
+                              uint8_t* rec_rows, int32_t* status, hipStream_t st);
+
 }  // namespace qfec

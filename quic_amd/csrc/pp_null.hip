@@ -451,6 +451,24 @@ __global__ __launch_bounds__(kAsmWaves * 64) void open_assemble_kernel(
     }
 }
 
+// After the decode: a group with an unfilled slot (row 255) is malformed whatever path
+// decoded it (the m = 1 XOR decode takes any row >= k as its parity block): status -3 and no
+// recovered rows.
+__global__ __launch_bounds__(kPPThreads) void open_status_kernel(long long groups, int k,
+                                                                 int rmax,
+                                                                 const uint8_t* __restrict__ rows,
+                                                                 uint8_t* rec_rows,
+                                                                 int32_t* status) {
+    const long long g = (long long)blockIdx.x * kPPThreads + threadIdx.x;
+    if (g >= groups) return;
+    const uint8_t* r = rows + g * k;
+    bool unfilled = false;
+    for (int i = 0; i < k; ++i) unfilled |= r[i] == 255;
+    if (!unfilled) return;
+    if (status) status[g] = -3;
+    for (int j = 0; j < rmax; ++j) rec_rows[g * rmax + j] = 255;
+}
+
 unsigned pp_grid(long long n) {
     return (unsigned)((n + kPPThreads - 1) / kPPThreads);
 }
@@ -539,6 +557,14 @@ hipError_t launch_open_groups(int form, int k, int m, int bb, long long groups,
            pkt_stride, pkt_len, ad_len, ad_all, blocks, open_len);
     qlaunch(open_assemble_kernel, dim3((unsigned)wg), dim3(kAsmWaves * 64), 0, st, k, m, bb,
             groups, pkt, pkt_stride, ad_len, ad_all, open_len, blocks, rows);
+    return hipGetLastError();
+}
+hipError_t launch_open_status(int k, int rmax, long long groups, const uint8_t* rows,
+                              uint8_t* rec_rows, int32_t* status, hipStream_t st) {
+    if (groups <= 0) return hipSuccess;
+    if (!pp_grid_ok(groups)) return hipErrorInvalidValue;
+    qlaunch(open_status_kernel, dim3(pp_grid(groups)), dim3(kPPThreads), 0, st, groups, k, rmax,
+            rows, rec_rows, status);
     return hipGetLastError();
 }
 #undef QPP_GO
