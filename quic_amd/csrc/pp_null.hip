@@ -195,6 +195,62 @@ __device__ __forceinline__ void span(H& h, Sink& s, const uint8_t* p, int len) {
     const u32x4* q = (const u32x4*)(p + head);
     const int rest = len - head;
     const int nc = rest >> 6;   // 64-byte chunks
+    // Line writer for the chunks: 16 source bytes make 4 output dwords d0..d3 (realigned by
+    // pb = ptr % 4 bytes with the carry), which land at dword positions di..di+3 of the
+    // output's 16-byte lines (di = the dword index of ptr - pb in its line, fixed for the
+    // span).  Rotated right by di they fill line L's positions di..3 and line L+1's 0..di-1:
+    // line L = (positions < di ? the previous rotation : this one), one 16-byte store; the
+    // first line is stored dword by dword from position di (the bytes before it are stored
+    // already or are not this writer's), the last partial line by flush_line.
+    const uint32_t pb = (uint32_t)(uintptr_t)s.ptr & 3u;
+    const uint32_t di = ((uint32_t)((uintptr_t)s.ptr - pb) >> 2) & 3u;
+    const uint32_t sh = 4u - pb;
+    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0;
+    auto eat4 = [&](const u32x4& v, bool first) {
+        if constexpr (HASH) {
+            h.word(v.x);
+            h.word(v.y);
+            h.word(v.z);
+            h.word(v.w);
+        }
+        if constexpr (WRITE) {
+            uint32_t d0 = v.x, d1 = v.y, d2 = v.z, d3 = v.w, nc4 = 0;
+            if (pb) {
+                d0 = (v.x << (8 * pb)) | s.carry;
+                d1 = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
+                d2 = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
+                d3 = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
+                nc4 = v.w >> (8 * sh);
+            }
+            // rotate right by di: R[j] = d[(j - di) & 3]
+            if (di & 1u) {
+                const uint32_t t = d3;
+                d3 = d2, d2 = d1, d1 = d0, d0 = t;
+            }
+            if (di & 2u) {
+                uint32_t t = d0;
+                d0 = d2, d2 = t;
+                t = d1, d1 = d3, d3 = t;
+            }
+            uint8_t* line = s.ptr - pb - 4 * di;
+            if (first) {
+                if (di <= 0) s.store_dw(line, d0);
+                if (di <= 1) s.store_dw(line + 4, d1);
+                if (di <= 2) s.store_dw(line + 8, d2);
+                s.store_dw(line + 12, d3);
+            } else {
+                u32x4 o;
+                o.x = di > 0 ? P0 : d0;
+                o.y = di > 1 ? P1 : d1;
+                o.z = di > 2 ? P2 : d2;
+                o.w = d3;
+                *(u32x4*)line = o;
+            }
+            P0 = d0, P1 = d1, P2 = d2, P3 = d3;
+            s.carry = nc4;
+            s.ptr += 16;
+        }
+    };
     u32x4 a[CH], b[CH];
     if (nc > 0) {
 #pragma unroll
@@ -205,8 +261,9 @@ __device__ __forceinline__ void span(H& h, Sink& s, const uint8_t* p, int len) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) b[u] = __builtin_nontemporal_load(q + CH * (j + 1) + u);
         }
+        eat4(a[0], j == 0);
 #pragma unroll
-        for (int u = 0; u < CH; ++u) eat(a[u]);
+        for (int u = 1; u < CH; ++u) eat4(a[u], false);
         if (j + 1 < nc) {
             if (j + 2 < nc) {
 #pragma unroll
@@ -214,9 +271,19 @@ __device__ __forceinline__ void span(H& h, Sink& s, const uint8_t* p, int len) {
                     a[u] = __builtin_nontemporal_load(q + CH * (j + 2) + u);
             }
 #pragma unroll
-            for (int u = 0; u < CH; ++u) eat(b[u]);
+            for (int u = 0; u < CH; ++u) eat4(b[u], false);
         }
     }
+    if constexpr (WRITE) {
+        // the line the chunks left open: positions 0 .. di - 1 hold P0 .. P(di - 1)
+        if (nc > 0) {
+            uint8_t* line = s.ptr - pb - 4 * di;
+            if (di > 0) s.store_dw(line, P0);
+            if (di > 1) s.store_dw(line + 4, P1);
+            if (di > 2) s.store_dw(line + 8, P2);
+        }
+    }
+    (void)P3;
     const u32x4* r = q + CH * nc;
     const int nr = (rest & 63) >> 4;
 #pragma unroll 1
