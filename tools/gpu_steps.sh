@@ -11,13 +11,13 @@
 #   preset:<k>,<m>        quick bench of a QuicR preset
 #   prof:<W>[:<args>]     rocprofv3 --kernel-trace --stats of a quick bench
 #   pmc:<W>[:<args>]      tools/pmc.sh passes (FETCH/WRITE traffic, waves, issue mix)
-# Extra args use ',' for spaces: quick:B:--opt,ring_nt=0.  GPU_STEPS_DRY=1 prints the steps.
+# Extra args use '+' for spaces: quick:B:--opt+ring_nt=0.  GPU_STEPS_DRY=1 prints the steps.
 export TMPDIR=/tmp
 specs=()
 for step in "$@"; do
   kind="${step%%:*}"; rest=""; [ "$step" != "$kind" ] && rest="${step#*:}"
   W="${rest%%:*}"; extra=""; [ "$rest" != "$W" ] && extra="${rest#*:}"
-  extra="${extra//,/ }"
+  extra="${extra//+/ }"
   tag=$(echo "$step" | tr -c 'A-Za-z0-9_\n' '_')
   quick="python bench.py --no-cpu-baseline --no-host --steps 10 --warmup 3"
   case "$kind" in
