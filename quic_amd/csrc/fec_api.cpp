@@ -494,7 +494,8 @@ int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
 // and D2H (s_out) are ordered by events, and NB staging buffers rotate, so the copy-in of
 // chunk i + 1 and the copy-out of chunk i - 1 overlap the kernels of chunk i (PCIe is
 // full duplex).  The kernels of all chunks stay on one stream, so the decode workspace is
-// never shared by two chunks in flight.  Chunk size: the host_chunk_mb option (64 MiB).
+// never shared by two chunks in flight.  Chunk size: the host_chunk_mb option (64 MiB), and
+// at least kHostMinChunkGroups groups.
 // fn(g0, n, buf, phase): phase 0 enqueues the H2D, 1 the kernels, 2 the D2H.
 template <class F>
 int host_pipeline_body(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
@@ -507,8 +508,15 @@ int host_pipeline_body(qfec_ctx* c, long long groups, size_t per_group, F&& fn) 
             QF_HIP(hipEventCreateWithFlags(&c->ev_out[b], hipEventDisableTiming));
         }
     }
+    // at least kHostMinChunkGroups groups per chunk (up to 2 GiB of staging per buffer): a
+    // 64 MiB chunk of D's 1.2 MB groups is 54 groups, too few to fill the device (D at
+    // 16,384 groups: 16.1 GiB/s with 64 MiB chunks, 22.9 with 256 MiB, 23.3 with 1 GiB)
+    constexpr long long kHostMinChunkGroups = 512;
     const size_t target = (size_t)std::max(1, c->tune.host_chunk_mb) << 20;
-    const long long chunk = std::max<long long>(1, std::min<long long>(groups, (long long)(target / per_group)));
+    const long long by_bytes = (long long)(target / per_group);
+    const long long floor_g = std::min<long long>(kHostMinChunkGroups, (long long)((2ull << 30) / per_group));
+    const long long chunk =
+        std::max<long long>(1, std::min<long long>(groups, std::max(by_bytes, floor_g)));
     const size_t bytes = (size_t)chunk * per_group + 16;
     for (int b = 0; b < qfec_ctx::NB; ++b) QF_HIP(c->pbuf[b].ensure(bytes));
     int i = 0;
