@@ -149,3 +149,16 @@ def test_every_host_kernel_stub_has_device_code():
         assert checked >= 5 and nhandles >= 100
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_grouped_packet_entry_points_reject_bad_arguments():
+    """qfec_seal_groups_batch / qfec_encode_seal_groups_batch / qfec_open_decode_batch
+    validate their arguments before any device access: a null context returns -2 (no GPU
+    call is made; the k + m limits need a context and are covered by the GPU tests)."""
+    L = _lib.load()
+    args_seal = (1, 1, 1352, 0, None, None, None, 0, None, 0, None, 1352, None, 1400, None,
+                 None)
+    assert L.qfec_seal_groups_batch(None, *args_seal) == -2
+    assert L.qfec_encode_seal_groups_batch(None, *args_seal) == -2
+    assert L.qfec_open_decode_batch(None, 10, 1, 1352, 0, None, 1400, None, None, 16, None,
+                                    None, None, None, None, None, None) == -2
