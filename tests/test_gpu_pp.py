@@ -355,3 +355,29 @@ def test_open_decode_full_size_a_shape(engine):
     assert bool((rr[:, 0][~lost_data] == 255).all())
     gi = torch.nonzero(lost_data).flatten()
     assert torch.equal(rec[gi, 0], data[gi, lose[gi]])
+
+
+def test_grouped_argument_limits(engine):
+    """k + m = 256 is a valid seal shape but not an open -> decode one (row tag 255 marks an
+    unfilled slot); a plaintext length above block_bytes is rejected; both with -2."""
+    import torch
+    from quic_amd.fec import FecError
+    G, k, m, bb = 1, 250, 6, 64
+    n = G * (k + m)
+    pkt = torch.zeros((n, 128), dtype=torch.uint8, device="cuda")
+    plen = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    blocks = torch.zeros((G, k, bb), dtype=torch.uint8, device="cuda")
+    rows = torch.zeros((G, k), dtype=torch.uint8, device="cuda")
+    ol = torch.zeros(n, dtype=torch.int32, device="cuda")
+    rec = torch.zeros((G, m, bb), dtype=torch.uint8, device="cuda")
+    rr = torch.zeros((G, m), dtype=torch.uint8, device="cuda")
+    with pytest.raises(FecError):
+        engine.open_decode(k, m, bb, pkt, plen, 16, blocks, rows, ol, rec, rr)
+    data = torch.zeros((G, 4, bb), dtype=torch.uint8, device="cuda")
+    par = torch.zeros((G, 2, bb), dtype=torch.uint8, device="cuda")
+    hdr = torch.zeros((6, 16), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((6, 128), dtype=torch.uint8, device="cuda")
+    olen = torch.zeros(6, dtype=torch.int32, device="cuda")
+    with pytest.raises(FecError):
+        engine.seal_groups(4, 2, bb, data, par, hdr, 16, bb + 1, out, olen)
+    torch.cuda.synchronize()
