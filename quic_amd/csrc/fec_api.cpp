@@ -303,11 +303,6 @@ int encode_impl(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
                                            c->tune));
         return 0;
     }
-    if (qfec::gf_tile_supported(k, m, bb, c->tune) && ((uintptr_t)d_data & 15) == 0) {
-        QF_HIP(qfec::launch_gf_tile_encode(d_data, d_par, k, m, bb, G, (long long)m * bb, st,
-                                           c->tune));
-        return 0;
-    }
     QF_HIP(qfec::launch_gf_encode(d_data, d_par, tab, k, m, bb, G, rc, st, c->tune));
     return 0;
 }
@@ -335,19 +330,12 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
     const long long tab_gstride = (long long)nchunk * k * std::max(rc, 4);
     const bool dcol = qfec::gf_dcol_supported(k, m, bb, c->tune) && rmax <= 16;
-    if ((dcol || qfec::gf_tile_syndrome_supported(k, m, bb, rmax, c->tune)) &&
-        ((uintptr_t)d_blocks & 15) == 0) {
+    if (dcol && ((uintptr_t)d_blocks & 15) == 0) {
         // compiled (128, 16) code: syndromes, then the r x r solve (reads precede stores
         // within a group, so in place needs no scratch)
         QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc,
                                         rmax, G, st, c->tune, nullptr, true));
-        if (dcol) {
-            QF_HIP(qfec::launch_gf_dcol_syndrome(d_blocks, d_out, w.coef, w.slots, w.nout, cenc,
-                                                 k, m, bb, G, rmax, tab_gstride, (long long)k * bb,
-                                                 st, c->tune));
-            return 0;
-        }
-        QF_HIP(qfec::launch_gf_tile_syndrome(d_blocks, d_out, w.coef, w.slots, w.nout, cenc, k,
+        QF_HIP(qfec::launch_gf_dcol_syndrome(d_blocks, d_out, w.coef, w.slots, w.nout, cenc, k,
                                              m, bb, G, rmax, tab_gstride, (long long)k * bb, st,
                                              c->tune));
         return 0;
@@ -437,19 +425,11 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
     if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
     qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
     const bool dcol = qfec::gf_dcol_supported(k, m, bb, c->tune) && rmax <= 16;
-    if ((dcol || qfec::gf_tile_syndrome_supported(k, m, bb, rmax, c->tune)) &&
-        ((uintptr_t)d_blocks & 15) == 0) {
+    if (dcol && ((uintptr_t)d_blocks & 15) == 0) {
         const int nchunk = (rmax + rc - 1) / rc;
         QF_HIP(qfec::launch_decode_prep(d_rows_in, nullptr, d_status, cenc, w, k, m, bb, rc, rmax,
                                         G, st, c->tune, d_rec_rows, true));
-        if (dcol) {
-            QF_HIP(qfec::launch_gf_dcol_syndrome(d_blocks, d_rec, w.coef, nullptr, w.nout, cenc, k,
-                                                 m, bb, G, rmax,
-                                                 (long long)nchunk * k * std::max(rc, 4),
-                                                 (long long)rmax * bb, st, c->tune));
-            return 0;
-        }
-        QF_HIP(qfec::launch_gf_tile_syndrome(d_blocks, d_rec, w.coef, nullptr, w.nout, cenc, k, m,
+        QF_HIP(qfec::launch_gf_dcol_syndrome(d_blocks, d_rec, w.coef, nullptr, w.nout, cenc, k, m,
                                              bb, G, rmax, (long long)nchunk * k * std::max(rc, 4),
                                              (long long)rmax * bb, st, c->tune));
         return 0;
@@ -495,7 +475,7 @@ int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
 // chunk i + 1 and the copy-out of chunk i - 1 overlap the kernels of chunk i (PCIe is
 // full duplex).  The kernels of all chunks stay on one stream, so the decode workspace is
 // never shared by two chunks in flight.  Chunk size: the host_chunk_mb option (64 MiB), and
-// at least kHostMinChunkGroups groups.
+// at least the host_min_groups option's groups (512).
 // fn(g0, n, buf, phase): phase 0 enqueues the H2D, 1 the kernels, 2 the D2H.
 template <class F>
 int host_pipeline_body(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
@@ -508,13 +488,14 @@ int host_pipeline_body(qfec_ctx* c, long long groups, size_t per_group, F&& fn) 
             QF_HIP(hipEventCreateWithFlags(&c->ev_out[b], hipEventDisableTiming));
         }
     }
-    // at least kHostMinChunkGroups groups per chunk (up to 2 GiB of staging per buffer): a
+    // at least host_min_groups groups per chunk (up to 2 GiB of staging per buffer): a
     // 64 MiB chunk of D's 1.2 MB groups is 54 groups, too few to fill the device (D at
-    // 16,384 groups: 16.1 GiB/s with 64 MiB chunks, 22.9 with 256 MiB, 23.3 with 1 GiB)
-    constexpr long long kHostMinChunkGroups = 512;
+    // 16,384 groups: 16.1 GiB/s with 64 MiB chunks, 22.9 with 256 MiB, 23.3 with 1 GiB).
+    // Both are options, so a caller (and the tests) can still force small chunks.
     const size_t target = (size_t)std::max(1, c->tune.host_chunk_mb) << 20;
     const long long by_bytes = (long long)(target / per_group);
-    const long long floor_g = std::min<long long>(kHostMinChunkGroups, (long long)((2ull << 30) / per_group));
+    const long long floor_g = std::min<long long>(std::max(1, c->tune.host_min_groups),
+                                                  (long long)((2ull << 30) / per_group));
     const long long chunk =
         std::max<long long>(1, std::min<long long>(groups, std::max(by_bytes, floor_g)));
     const size_t bytes = (size_t)chunk * per_group + 16;
@@ -619,22 +600,20 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"xor_slots", &t.xor_slots, 2, 4},     {"xor_waves", &t.xor_waves, 1, 4},
         {"dma", &t.dma, 0, 1},                 {"stream", &t.stream, 0, 1},
         {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
-        {"const_enc", &t.const_enc, 0, 1},     {"tile", &t.tile, 0, 1},
-        {"stream_static", &t.stream_static, 0, 1},
-        {"tile_grid", &t.tile_grid, 0, 1 << 20}, {"tile_depth", &t.tile_depth, 4, 6}, {"tile_pair", &t.tile_pair, 0, 1},
-        {"tile_occ2", &t.tile_occ2, 0, 1},
+        {"const_enc", &t.const_enc, 0, 1},     {"stream_static", &t.stream_static, 0, 1},
+        {"dcol_grid", &t.dcol_grid, 0, 1 << 20},
         {"bsyn", &t.bsyn, 0, 1},               {"dcol", &t.dcol, 0, 1},
         {"dcol_cache", &t.dcol_cache, 0, 3},     {"stream_rc16", &t.stream_rc16, 0, 1},
         {"ring_nt", &t.ring_nt, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
+        {"host_min_groups", &t.host_min_groups, 1, 1 << 20},
         {"pp_hash", &c->pp_hash, 0, 1},
     };
     for (const Opt& o : opts) {
         if (strcmp(o.n, name) != 0) continue;
-        if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))) ||
-            (o.p == &t.tile_depth && value == 5 && !t.tile_occ2))
+        if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))))
             return fail(-2, std::string("option value out of range: ") + name);
         *o.p = value;
         return 0;
@@ -649,12 +628,12 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
     const std::pair<const char*, int> opts[] = {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
-        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"tile", t.tile}, {"tile_grid", t.tile_grid},
-        {"tile_depth", t.tile_depth}, {"tile_pair", t.tile_pair}, {"tile_occ2", t.tile_occ2},
+        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"dcol_grid", t.dcol_grid},
         {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol}, {"dcol_cache", t.dcol_cache}, {"stream_rc16", t.stream_rc16},
         {"ring_nt", t.ring_nt},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
-        {"host_chunk_mb", t.host_chunk_mb}, {"pp_hash", c->pp_hash},
+        {"host_chunk_mb", t.host_chunk_mb}, {"host_min_groups", t.host_min_groups},
+        {"pp_hash", c->pp_hash},
     };
     for (const auto& o : opts)
         if (strcmp(o.first, name) == 0) { *value = o.second; return 0; }

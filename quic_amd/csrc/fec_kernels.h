@@ -26,12 +26,6 @@ struct Tune {
     int stream_grid = 0;      // gf_stream: grid cap in workgroups (0: CUs x per-CU fit)
     int stream_static = 1;    // gf_stream: compile-time ring schedule for k = 32, bb = 1352
     int const_enc = 1;        // encode kernels specialised for fixed (k, m) where compiled
-    int tile = 1;             // (128, 16) x 9008 B: gf_tile / gf_tile_syn (0: gf_apply)
-    int tile_grid = 0;        // gf_tile: grid cap in workgroups (0: CUs x per-CU fit)
-    int tile_depth = 6;       // gf_tile: blocks in flight per workgroup (4 or 6)
-    int tile_pair = 1;        // gf_tile encode: one workgroup barrier per two blocks (depth >= 5)
-    int tile_occ2 = 0;        // gf_tile encode: two workgroups per CU (<= 96 VGPRs, no
-                              //   register double buffer; depth 5 with pairs, or 4 / 6)
     int pd = 2;               // gf_apply: register pipeline depth (1..3)
     int flat = 1;             // gf_apply: lane-flat encode
     int enc_rc = 8;           // gf_apply: encode outputs per wave (2, 4, 8)
@@ -40,7 +34,8 @@ struct Tune {
                               //   (0: the run-time gf_stream decode)
     int bsyn_depth = 5;       // gf_bsyn: blocks in flight per wave (3..7)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16
-                              //   rows; 0: gf_tile / gf_tile_syn)
+                              //   rows; 0: gf_apply)
+    int dcol_grid = 0;        // gf_dcol: grid cap in workgroups (0: CUs x per-CU fit)
     int dcol_cache = 2;       // gf_dcol cache policy: encode 0 / 1 cached loads and non-temporal
                               //   stores, 2 / 3 cached loads and stores; decode (stores
                               //   plain) non-temporal loads for 0 / 2, cached 1 / 3
@@ -48,6 +43,8 @@ struct Tune {
                               //   units of 8, the second empty for <= 8 losses and skipped)
     int ring_nt = 1;          // gf_ring (B/C encode) parity stores non-temporal (0: plain)
     int host_chunk_mb = 64;   // host-pointer batches: chunk size
+    int host_min_groups = 512;  // host-pointer batches: at least this many groups per chunk
+                                //   (capped at 2 GiB of staging per buffer)
 };
 
 // Records the name of a kernel a call launched (qfec_last_kernels(), per thread).
@@ -91,7 +88,7 @@ struct DecodeWork {
     int32_t* nout;     // [G]                  number of recovered blocks in this group
 };
 
-// Syndrome table (decode prep in syndrome mode, read by gf_tile's syndrome decode), one per
+// Syndrome table (decode prep in syndrome mode, read by gf_dcol's syndrome decode), one per
 // group at coef + g * coef_gstride, k <= 128 and at most 16 parity rows:
 namespace syn {
 constexpr int kPerm = 0;     // u8[k]  stream order of the slots: the present data rows
@@ -196,20 +193,6 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
                             long long out_gstride, bool decode, hipStream_t st,
                             const Tune& t);
 
-
-// Workgroup-shared LDS block stream for 9008-byte blocks, column-tile waves (gf_tile.hip):
-// encode of the compiled (128, 16) code.
-bool gf_tile_supported(int k, int m, int bb, const Tune& t);
-hipError_t launch_gf_tile_encode(const uint8_t* in, uint8_t* out, int k, int m, int bb,
-                                 long long groups, long long out_gstride, hipStream_t st,
-                                 const Tune& t);
-// Syndrome decode of the compiled (128, 16) code from the syn:: table (gf_tile.hip).
-bool gf_tile_syndrome_supported(int k, int m, int bb, int rmax, const Tune& t);
-hipError_t launch_gf_tile_syndrome(const uint8_t* in, uint8_t* out, const uint8_t* tab,
-                                   const uint8_t* slots, const int32_t* nout,
-                                   const uint8_t* cenc, int k, int m, int bb, long long groups,
-                                   int rmax, long long tab_gstride, long long out_gstride,
-                                   hipStream_t st, const Tune& t);
 
 // One wave per column tile computing all 16 rows (gf_dcol.hip): encode of the compiled
 // (128, 16) x 9008-byte code, and its syndrome decode from the syn:: table.

@@ -512,7 +512,7 @@ static unsigned dcol_grid(long long groups, const Tune& t, size_t lds) {
     // two workgroups of 4 waves per CU (two waves per SIMD at <= 256 VGPRs), LDS permitting
     const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
     long long cap = (long long)t.cus * per_cu;
-    if (t.tile_grid > 0) cap = t.tile_grid;          // tests: many units per wave
+    if (t.dcol_grid > 0) cap = t.dcol_grid;          // tests: many units per wave
     return (unsigned)std::min<long long>(want, cap);
 }
 

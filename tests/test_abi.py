@@ -109,46 +109,61 @@ def test_timing_events_hook_arguments():
 
 def test_every_host_kernel_stub_has_device_code():
     """Each kernel a host object registers has a device entry (its .kd descriptor) in the
-    same object's gfx950 code object.  A host pass and a device pass of one source that see
-    different file contents (an edit during a build) leave a stub the runtime cannot
-    resolve: `Cannot find Symbol` and an abort at the first launch."""
+    same object's gfx950 code object (tools/check_stubs.py, which `make lib` also runs).  A
+    host pass and a device pass of one source that see different file contents (an edit
+    during a build) leave a stub the runtime cannot resolve: `Cannot find Symbol` and an
+    abort at the first launch."""
     import glob
-    import shutil
-    import subprocess
-    import tempfile
-    llvm = "/opt/rocm/lib/llvm/bin"
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_stubs
     objs = sorted(glob.glob(os.path.join(ROOT, "build", "*.o")))
-    if not objs or not os.path.exists(os.path.join(llvm, "llvm-readelf")):
+    if not objs or not os.path.exists(os.path.join(check_stubs.LLVM, "llvm-readelf")):
         pytest.skip("no build objects or no ROCm llvm tools")
-    tmp = tempfile.mkdtemp()
-    try:
-        checked = nhandles = 0
-        for o in objs:
-            fat = os.path.join(tmp, "fat.bin")
-            r = subprocess.run([os.path.join(llvm, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}",
-                                o, os.path.join(tmp, "scratch.o")], capture_output=True)
-            if r.returncode != 0 or not os.path.exists(fat):
-                continue                                  # host-only object
-            co = os.path.join(tmp, "dev.co")
-            subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", "--type=o",
-                            f"--input={fat}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
-                            f"--output={co}"], check=True, capture_output=True)
-            dev = subprocess.run([os.path.join(llvm, "llvm-readelf"), "-s", co], check=True,
-                                 capture_output=True, text=True).stdout
-            kd = {ln.split()[-1][:-3] for ln in dev.splitlines() if ln.strip().endswith(".kd")}
-            host = subprocess.run([os.path.join(llvm, "llvm-readelf"), "-s", "-W", o], check=True,
-                                  capture_output=True, text=True).stdout
-            # a kernel's host handle is an 8-byte OBJECT named exactly like the device entry
-            stubs = {ln.split()[-1] for ln in host.splitlines()
-                     if " OBJECT " in ln and " UND " not in ln and "_kernel" in ln.split()[-1]}
-            missing = sorted(stubs - kd)
-            assert not missing, f"{os.path.basename(o)}: host stubs without device code: {missing}"
-            os.remove(fat)
-            checked += 1
-            nhandles += len(stubs)
-        assert checked >= 5 and nhandles >= 100
-    finally:
-        shutil.rmtree(tmp, ignore_errors=True)
+    bad, n = check_stubs.check(objs)
+    assert not bad, bad
+    assert n >= 100
+
+
+_STUB_SRC = r"""
+#include <hip/hip_runtime.h>
+#if defined(__HIP_DEVICE_COMPILE__) && defined(MISMATCH)
+__global__ void probe_dev_kernel(int* p) { *p = 2; }     // the device pass sees another file
+#else
+__global__ void probe_kernel(int* p) { *p = 1; }
+#endif
+#if !defined(__HIP_DEVICE_COMPILE__)
+extern "C" void probe_launch(int* p) { hipLaunchKernelGGL(probe_kernel, 1, 1, 0, 0, p); }
+#endif
+"""
+
+
+@pytest.mark.parametrize("mismatch", [False, True])
+def test_make_lib_refuses_a_stub_without_device_code(tmp_path, mismatch):
+    """The Makefile's link rule runs the stub check: an object whose host pass registers a
+    kernel its device pass does not contain fails `make` and leaves no library behind; a
+    consistent object links."""
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    src = tmp_path / "probe.hip"
+    src.write_text(_STUB_SRC)
+    obj = tmp_path / "probe.o"
+    flags = ["-Xarch_device", "-DMISMATCH"] if mismatch else []
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O1", "-fPIC", *flags, "-c", str(src),
+                    "-o", str(obj)], check=True, capture_output=True)
+    lib = tmp_path / "libprobe.so"
+    lib.write_bytes(b"stale")      # a library from an earlier build must not survive a failure
+    os.utime(lib, (0, 0))          # older than the object: make relinks it
+    r = subprocess.run(["make", "-s", "-f", os.path.join(ROOT, "Makefile"), f"LIB={lib}",
+                        f"OBJS={obj}", str(lib)], capture_output=True, text=True)
+    if mismatch:
+        assert r.returncode != 0
+        assert "without device code" in r.stderr and "probe_kernel" in r.stderr
+        assert not lib.exists()
+    else:
+        assert r.returncode == 0, r.stderr
+        assert lib.exists() and lib.read_bytes()[:4] == b"\x7fELF"
 
 
 def test_grouped_packet_entry_points_reject_bad_arguments():

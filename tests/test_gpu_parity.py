@@ -339,6 +339,43 @@ def test_decode_recovered_host(engine, oracle):
     assert st.abs().max() == 0
 
 
+@pytest.mark.parametrize("k,m,r", [(32, 4, 3), (10, 10, 7)])
+def test_host_pipeline_many_chunks(tuned_engine, oracle, k, m, r):
+    """Host-pointer batches cut into more chunks than the NB = 3 rotating staging buffers
+    (host_chunk_mb = 1, host_min_groups = 1: 1 MiB chunks): every buffer is reused, so the
+    H2D / kernel / D2H event chain must order each reuse after the previous chunk's
+    copy-out.  Encode, in-place decode and recovered-blocks decode against the oracle."""
+    import torch
+    engine = tuned_engine
+    engine.set_option("host_chunk_mb", 1)
+    engine.set_option("host_min_groups", 1)
+    bb = 1352
+    G = 4 * ((3 << 20) // (2 * k * bb)) + 5       # more than 4 x NB chunks for every call
+    data = synth.group_data(900 + k, k, bb, G)
+    p_or, _ = oracle.encode_batch(k, m, bb, data)
+    par, rc = engine.encode_host(k, m, bb, data)
+    assert rc == 0
+    np.testing.assert_array_equal(par, p_or)
+    rows, src = synth.loss_patterns(k, m, r, G, 31 + k, shuffle=True)
+    recv = synth.assemble_received(data, p_or, src)
+    b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
+    b, rr, s = engine.decode_host(k, m, bb, recv, rows)
+    np.testing.assert_array_equal(s, s_or)
+    np.testing.assert_array_equal(rr, r_or)
+    np.testing.assert_array_equal(b, b_or)
+    exp, exp_rows = expected_recovered(k, m, bb, rows, b_or, r_or, s_or)
+    rmax = min(k, m)
+    rec = torch.zeros((G, rmax, bb), dtype=torch.uint8)
+    rec_rows = torch.zeros((G, rmax), dtype=torch.uint8)
+    st = torch.full((G,), 7, dtype=torch.int32)
+    fec.decode_recovered_host_into(engine, k, m, bb, torch.from_numpy(recv),
+                                   torch.from_numpy(rows), rec, rec_rows, st)
+    np.testing.assert_array_equal(rec_rows.numpy(), exp_rows)
+    mask = exp_rows != 255
+    np.testing.assert_array_equal(rec.numpy()[mask], exp[mask])
+    assert st.abs().max() == 0
+
+
 # ------------------------------------------- gf_stream ring (many groups per wave)
 @pytest.fixture
 def tuned_engine():
@@ -421,12 +458,9 @@ OPTION_SETS = [
     {"xor_slots": 3, "xor_waves": 3}, {"xor_slots": 4, "xor_waves": 2}, {"xor_waves": 1},
     {"dma": 0}, {"stream": 0}, {"stream": 0, "pd": 1}, {"stream": 0, "pd": 3},
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
-    {"stream_ring": 36}, {"host_chunk_mb": 1}, {"const_enc": 0}, {"tile": 0},
-    {"tile_depth": 4}, {"tile_pair": 0}, {"stream_static": 0},
-    {"tile_occ2": 1, "tile_depth": 5}, {"tile_occ2": 1, "tile_depth": 6, "tile_pair": 0},
-    {"tile_occ2": 1, "tile_depth": 4, "tile_pair": 0}, {"bsyn": 0}, {"bsyn_depth": 3},
-    {"dcol": 0}, {"dcol": 0, "tile_occ2": 1, "tile_depth": 5}, {"dcol_cache": 0},
-    {"dcol_cache": 1}, {"dcol_cache": 3},
+    {"stream_ring": 36}, {"host_chunk_mb": 1, "host_min_groups": 1}, {"const_enc": 0},
+    {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 3}, {"dcol": 0}, {"dcol_cache": 0},
+    {"dcol_cache": 1}, {"dcol_cache": 3}, {"stream_rc16": 1}, {"ring_nt": 0},
 ]
 
 
@@ -782,28 +816,22 @@ def test_bsyn_decode_patterns(tuned_engine, oracle, depth, grid):
     np.testing.assert_array_equal(b, recv[~ok])
 
 
-# ------------------------------------------------- gf_tile (9008-byte blocks, config D)
+# ------------------------------------------------- gf_dcol (9008-byte blocks, config D)
 D_KERNELS = {1: ("gf_dcol_kernel<encode,k128m16>", "gf_dcol_kernel<decode,k128m16>"),
-             0: ("gf_tile_kernel<encode,k128m16", "gf_tile_syn_kernel<decode,k128m16>")}
+             0: ("gf_apply_kernel<encode", "gf_apply_kernel<decode")}
 
 
 @pytest.mark.parametrize("dcol", [1, 0])
-@pytest.mark.parametrize("depth", [4, 6, "6p"])
 @pytest.mark.parametrize("grid", [1, 3, 0])
 @pytest.mark.parametrize("k,m,r", [(128, 16, 8), (128, 16, 13), (40, 16, 16), (16, 6, 4)])
-def test_tile_many_groups_per_workgroup(tuned_engine, oracle, depth, grid, k, m, r, dcol):
+def test_tile_many_groups_per_workgroup(tuned_engine, oracle, grid, k, m, r, dcol):
     """Config D's kernels with the grid capped so one workgroup streams several groups back
     to back (the DMA prefetch crosses group / unit boundaries and the previous group's stores
     sit in the vmcnt count); every third group has no loss.  dcol = 1: gf_dcol (one wave
-    per column tile, units of (group, tile)); dcol = 0: gf_tile / gf_tile_syn (depth
-    options)."""
-    if dcol and depth != 6:
-        pytest.skip("gf_dcol has no depth options")
+    per column tile, units of (group, tile)); dcol = 0: the gf_apply fallback."""
     engine = tuned_engine
     engine.set_option("dcol", dcol)
-    engine.set_option("tile_grid", grid)
-    engine.set_option("tile_depth", 6 if depth == "6p" else depth)
-    engine.set_option("tile_pair", 1 if depth == "6p" else 0)   # one barrier per 2 blocks
+    engine.set_option("dcol_grid", grid)
     bb, G = 9008, 7
     data = synth.group_data(4000 + k + m + grid, k, bb, G)
     p_or, rc_or = oracle.encode_batch(k, m, bb, data)
@@ -849,7 +877,7 @@ def check_decodes(engine, oracle, k, m, bb, recv, rows, dec_kernel):
 @pytest.mark.parametrize("grid", [1, 3, 0])
 def test_syndrome_decode_patterns(tuned_engine, oracle, grid, dcol):
     """Config D's decode (syndromes of the compiled (128, 16) code, then the r x r solve,
-    gf_tile_syn_kernel) on hand-built receive sets: no loss, 16 losses, single and scattered
+    gf_dcol_kernel; dcol = 0: the gf_apply fallback) on hand-built receive sets: no loss, 16 losses, single and scattered
     parity rows, more than 8 losses (two syndrome exchange rounds), a repeated data row (an
     extra block with run-time coefficients); shuffled arrival; the grid capped so groups
     share workgroups.  Malformed sets (a repeated parity row: singular; a row tag past
@@ -857,7 +885,7 @@ def test_syndrome_decode_patterns(tuned_engine, oracle, grid, dcol):
     singular bit matrix / reads past its Cauchy matrix): status -3, group left unchanged."""
     engine = tuned_engine
     engine.set_option("dcol", dcol)
-    engine.set_option("tile_grid", grid)
+    engine.set_option("dcol_grid", grid)
     k, m, bb = 128, 16, 9008
     rng = np.random.default_rng(90 + grid)
     data = synth.group_data(777 + grid, k, bb, 10)

@@ -1,8 +1,7 @@
 """ISA guard for the counted-vmcnt kernels (CPU only: hipcc cross-compiles gfx950).
 
-gf_stream_kernel / gf_ring_kernel (quic_amd/csrc/gf_stream.hip) and gf_tile_kernel /
-gf_tile_syn_kernel (gf_tile.hip) keep their
-own count of the VMEM instructions they issued and wait with `s_waitcnt vmcnt(N)` for
+gf_stream_kernel / gf_ring_kernel (quic_amd/csrc/gf_stream.hip), gf_bsyn_kernel (gf_bsyn.hip)
+and gf_dcol_kernel (gf_dcol.hip) keep their own count of the VMEM instructions they issued and wait with `s_waitcnt vmcnt(N)` for
 exactly the pieces a block needs.  That is only sound if the compiler emits no VMEM
 instruction outside the count (a global_load of a uniform byte, a register spill, say) and
 inserts no vmcnt wait of its own (which would drain the pipeline).  This test compiles the
@@ -20,7 +19,7 @@ COUNTED = {"global_load_lds_dwordx4", "buffer_load_dwordx4", "buffer_store_dword
 DMA = ("global_load_lds_dwordx4", "buffer_load_dwordx4")   # the latter only as `... lds`
 
 
-@pytest.fixture(scope="module", params=["gf_stream", "gf_tile", "gf_bsyn", "gf_dcol"])
+@pytest.fixture(scope="module", params=["gf_stream", "gf_bsyn", "gf_dcol"])
 def stream_isa(tmp_path_factory, request):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
