@@ -247,7 +247,7 @@ int get_cenc(qfec_ctx* c, int k, int m, const uint8_t** out) {
         if (cauchy_rows(k, m, t.data() + k)) return fail(-1, "no Cauchy matrix for (k, m)");
     }
     auto buf = std::make_unique<DevBuf>();
-    QF_HIP(buf->ensure(t.size()));
+    QF_HIP(buf->ensure(t.size() + 16));   // dword loads of the last row stay in the buffer
     QF_HIP(hipMemcpy(buf->p, t.data(), t.size(), hipMemcpyHostToDevice));
     *out = (const uint8_t*)buf->p;
     c->cenc_tab.emplace(key, std::move(buf));
@@ -258,7 +258,8 @@ int decode_workspace(qfec_ctx* c, int k, int rmax, int rc, long long groups) {
     const int rcp = std::max(rc, 4);
     const int nchunk = (rmax + rc - 1) / rc;
     // per group: the apply coefficients, or a syndrome table (bsyn:: / syn::)
-    const size_t per = std::max<size_t>((size_t)nchunk * k * rcp, qfec::bsyn::kBytes);
+    const size_t per = std::max<size_t>({(size_t)nchunk * k * rcp, (size_t)qfec::bsyn::kBytes,
+                                         (size_t)qfec::psyn::kBytes});
     QF_HIP(c->dcoef.ensure((size_t)groups * per));
     QF_HIP(c->dslots.ensure((size_t)groups * rmax));
     QF_HIP(c->dnout.ensure((size_t)groups * sizeof(int32_t)));
@@ -338,6 +339,15 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
         QF_HIP(qfec::launch_gf_dcol_syndrome(d_blocks, d_out, w.coef, w.slots, w.nout, cenc, k,
                                              m, bb, G, rmax, tab_gstride, (long long)k * bb, st,
                                              c->tune));
+        return 0;
+    }
+    if (qfec::gf_psyn_supported(k, m, bb, rmax, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
+        // compiled QuicR preset code: syndromes of every parity row, then Gauss-Jordan in
+        // place (a group's stores follow all of its reads: in place needs no scratch)
+        QF_HIP(qfec::launch_decode_prep_psyn(d_rows_in, d_rows_out, d_status, cenc, w.coef,
+                                             w.slots, w.nout, nullptr, k, m, bb, rmax, G, st));
+        QF_HIP(qfec::launch_gf_psyn(d_blocks, d_out, w.coef, cenc, w.slots, w.nout, k, m, bb, G,
+                                    rmax, (long long)k * bb, st, c->tune));
         return 0;
     }
     if (qfec::gf_bsyn_supported(k, m, bb, rmax, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
@@ -432,6 +442,13 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
         QF_HIP(qfec::launch_gf_dcol_syndrome(d_blocks, d_rec, w.coef, nullptr, w.nout, cenc, k, m,
                                              bb, G, rmax, (long long)nchunk * k * std::max(rc, 4),
                                              (long long)rmax * bb, st, c->tune));
+        return 0;
+    }
+    if (qfec::gf_psyn_supported(k, m, bb, rmax, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
+        QF_HIP(qfec::launch_decode_prep_psyn(d_rows_in, nullptr, d_status, cenc, w.coef, w.slots,
+                                             w.nout, d_rec_rows, k, m, bb, rmax, G, st));
+        QF_HIP(qfec::launch_gf_psyn(d_blocks, d_rec, w.coef, cenc, nullptr, w.nout, k, m, bb, G,
+                                    rmax, (long long)rmax * bb, st, c->tune));
         return 0;
     }
     if (qfec::gf_bsyn_supported(k, m, bb, rmax, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
@@ -605,6 +622,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"bsyn", &t.bsyn, 0, 1},               {"dcol", &t.dcol, 0, 1},
         {"dcol_cache", &t.dcol_cache, 0, 3},     {"stream_rc16", &t.stream_rc16, 0, 1},
         {"ring_nt", &t.ring_nt, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
+        {"psyn", &t.psyn, 0, 1},               {"psyn_depth", &t.psyn_depth, 5, 9},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -630,7 +648,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
         {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"dcol_grid", t.dcol_grid},
         {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol}, {"dcol_cache", t.dcol_cache}, {"stream_rc16", t.stream_rc16},
-        {"ring_nt", t.ring_nt},
+        {"ring_nt", t.ring_nt}, {"psyn", t.psyn}, {"psyn_depth", t.psyn_depth},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb}, {"host_min_groups", t.host_min_groups},
         {"pp_hash", c->pp_hash},

@@ -33,6 +33,9 @@ struct Tune {
     int bsyn = 1;             // (32, 4) x 1352 B decode: compiled syndrome kernel gf_bsyn
                               //   (0: the run-time gf_stream decode)
     int bsyn_depth = 5;       // gf_bsyn: blocks in flight per wave (3..7)
+    int psyn = 1;             // QuicR presets with m >= 7 at 1352 B: compiled syndrome decode
+                              //   gf_psyn (0: the run-time gf_stream decode)
+    int psyn_depth = 7;       // gf_psyn: blocks in flight per wave (5, 7, 9)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16
                               //   rows; 0: gf_apply)
     int dcol_grid = 0;        // gf_dcol: grid cap in workgroups (0: CUs x per-CU fit)
@@ -116,6 +119,18 @@ constexpr int kSinv = 76;    // u8[4][4] Sinv[j][i]: recovered j = sum_i Sinv[j]
 constexpr int kERow = 92;    // u8[64] row tag of extra e (255: no-op, unchanged group)
 constexpr int kBytes = 156;
 }  // namespace bsyn
+
+// Preset syndrome table (decode_prep_psyn, read by gf_psyn), one per group at
+// tab + g * kBytes, k <= 64, m <= 32, at most 16 recovered blocks:
+namespace psyn {
+constexpr int kPerm = 0;     // u8[64] stream order of the slots: present data rows ascending
+                             //        (first copy of each), then the extras in slot order
+constexpr int kMask = 64;    // u32[2] bit x: data row x is in the ascending part
+constexpr int kYs = 72;      // u8[16] received parity rows, ascending (syndrome slot s)
+constexpr int kERow = 88;    // u8[64] row tag of extra e (255: no-op, unchanged group)
+constexpr int kCoef = 152;   // u8[16][16] g[p][i]: pivot p's coefficient for slot i
+constexpr int kBytes = 408;
+}  // namespace psyn
 
 // parity[g*out_gstride ..+bb) = XOR of the k blocks of group g (m == 1 encode, and the
 // P0 the reference writes before rejecting invalid m > 1 parameters).
@@ -214,6 +229,19 @@ hipError_t launch_decode_prep_bsyn(const uint8_t* rows_in, uint8_t* rows_out, in
                                    int32_t* nout, uint8_t* rec_rows, int k, int m, int bb,
                                    int rmax, long long groups, hipStream_t st);
 hipError_t launch_gf_bsyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
+                          const uint8_t* cenc, const uint8_t* slots, const int32_t* nout, int k,
+                          int m, int bb, long long groups, int rmax, long long out_gstride,
+                          hipStream_t st, const Tune& t);
+
+// Syndrome decode of the compiled QuicR preset codes with m >= 7 at 1352-byte blocks
+// (gf_psyn.hip): prep (psyn:: table, 16 lanes per group) and the block pass + in-place
+// Gauss-Jordan replay.
+bool gf_psyn_supported(int k, int m, int bb, int rmax, const Tune& t);
+hipError_t launch_decode_prep_psyn(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
+                                   const uint8_t* cenc, uint8_t* tab, uint8_t* slots,
+                                   int32_t* nout, uint8_t* rec_rows, int k, int m, int bb,
+                                   int rmax, long long groups, hipStream_t st);
+hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
                           const uint8_t* cenc, const uint8_t* slots, const int32_t* nout, int k,
                           int m, int bb, long long groups, int rmax, long long out_gstride,
                           hipStream_t st, const Tune& t);

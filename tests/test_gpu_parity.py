@@ -729,17 +729,24 @@ def test_stream_any_small_block(engine, oracle, bb, k, m, r):
 PRESETS = [(5, 5), (10, 10), (10, 15), (10, 20), (15, 15), (250, 5)]   # quic_fec_group.cc:22-82
 
 
-@pytest.mark.parametrize("grid", [0, 1])
+PSYN = {(10, 10), (10, 15), (10, 20), (15, 15)}   # m >= 7: gf_psyn's compiled syndrome decode
+
+
+@pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0, "stream_rc16": 1}],
+                         ids=["default", "grid1", "runtime_rc16"])
 @pytest.mark.parametrize("k,m", PRESETS)
-def test_reference_presets_stream(tuned_engine, oracle, k, m, grid):
+def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
     """QuicR's negotiated configurations with 1350-byte payloads (bb = 1352): odd k puts every
-    other group 8 bytes off a 16-byte boundary, m > 8 and more than 8 losses cut the outputs
-    into chunks (units of one group each).  All of them run gf_stream, never gf_apply;
-    bit-exact vs the oracle in every decode layout, with as many losses as the code allows
-    (min(k, m)) and with one; grid 1: one workgroup streams every unit."""
-    import torch
+    other group 8 bytes off a 16-byte boundary, m > 8 and more than 8 losses cut the run-time
+    decode's outputs into chunks.  Encodes run the compiled gf_stream; decodes run gf_psyn
+    (compiled syndromes + Gauss-Jordan) for the m >= 7 presets and gf_stream for the others,
+    never gf_apply; with psyn = 0 and stream_rc16 = 1, the run-time gf_stream decode in one
+    16-block unit.  Bit-exact vs the oracle in every decode layout, with as many losses as
+    the code allows (min(k, m)), with half of them and with one; grid 1: one workgroup
+    streams every unit."""
     engine = tuned_engine
-    engine.set_option("stream_grid", grid)
+    for name, v in opts.items():
+        engine.set_option(name, v)
     bb, G = 1352, 11
     data = synth.group_data(9000 + k + m, k, bb, G)
     p_or, rc_or = oracle.encode_batch(k, m, bb, data)
@@ -747,12 +754,78 @@ def test_reference_presets_stream(tuned_engine, oracle, k, m, grid):
     assert fec.last_kernels().startswith("gf_stream_kernel<encode"), fec.last_kernels()
     assert rc == rc_or == 0
     np.testing.assert_array_equal(p_gpu, p_or)
-    for r in (min(k, m), 1):
+    dec = ("gf_psyn_kernel<decode" if (k, m) in PSYN and opts.get("psyn", 1)
+           else "gf_stream_kernel<decode")
+    for r in sorted({min(k, m), min(k, m) // 2, 1}):
         rows, src = synth.loss_patterns(k, m, r, G, 31 + r, shuffle=True)
         recv = synth.assemble_received(data, p_or, src)
-        s_or = check_decodes(engine, oracle, k, m, bb, recv, rows, "gf_stream_kernel<decode")
+        s_or = check_decodes(engine, oracle, k, m, bb, recv, rows, dec)
         assert (s_or == 0).all()
         assert "gf_apply" not in fec.last_kernels()
+
+
+@pytest.mark.parametrize("depth", [5, 7, 9])
+@pytest.mark.parametrize("grid", [1, 2, 0])
+@pytest.mark.parametrize("k,m", sorted(PSYN))
+def test_psyn_decode_patterns(tuned_engine, oracle, k, m, depth, grid):
+    """The preset decode (gf_psyn: syndromes of every parity row with the compiled code,
+    Gauss-Jordan replayed on the data) on hand-built receive sets: no loss, 1 .. min(k, m)
+    losses with first / scattered / last parity rows in any arrival order (blocks streamed
+    from any slot, odd slots of odd-k groups 8 bytes off a 16-byte boundary), a repeated
+    data row (an extra block with run-time coefficients), malformed sets (a repeated parity
+    row: singular; a row tag past k + m: status -3, group unchanged); the grid capped so a
+    wave streams many groups back to back (the next group's blocks are prefetched across
+    the previous group's stores, up to 16 x 2 x min(k, m) of them)."""
+    engine = tuned_engine
+    engine.set_option("stream_grid", grid)
+    engine.set_option("psyn_depth", depth)
+    bb = 1352
+    rmax = min(k, m)
+    rng = np.random.default_rng(500 + 7 * k + m + depth + grid)
+    G = 26
+    data = synth.group_data(1901 + k + m + depth + grid, k, bb, G)
+    p_or, _ = oracle.encode_batch(k, m, bb, data)
+
+    def lose(lost, par):
+        keep = [x for x in range(k) if x not in set(lost)]
+        return keep + [k + y for y in par]
+    base = [
+        list(range(k)),
+        lose([0], [0]), lose([k - 1], [m - 1]), lose([3], [m // 2]),
+        lose(list(range(rmax)), list(range(rmax))),
+        lose(list(range(k - rmax, k)), list(range(m - rmax, m))),
+        lose(sorted(rng.choice(k, rmax, replace=False)), sorted(rng.choice(m, rmax, replace=False))),
+        lose([1, 4], [m - 1, 0]),
+    ]
+    dup = list(range(k))                      # row 6 twice, row 5 missing, parity row 2
+    dup[5] = 6
+    dup[7] = k + 2
+    sets = base + [dup]
+    while len(sets) < G - 2:
+        r = int(rng.integers(0, rmax + 1))
+        sets.append(lose(sorted(rng.choice(k, r, replace=False)),
+                         sorted(rng.choice(m, r, replace=False))))
+    rows = np.zeros((G, k), np.uint8)
+    src = np.zeros((G, k), np.int16)
+    for g, st in enumerate(sets):
+        st = np.array(st)
+        if g % 2:
+            st = st[rng.permutation(k)]
+        rows[g] = st
+        src[g] = st
+    recv = synth.assemble_received(data[:G - 2], p_or[:G - 2], src[:G - 2])
+    ok_rows = rows[:G - 2]
+    s_or = check_decodes(engine, oracle, k, m, bb, recv, ok_rows, "gf_psyn_kernel<decode")
+    assert (s_or == 0).all()
+    # malformed: a repeated parity row (singular), a row tag past k + m
+    bad = np.stack([np.array(lose([2, 3], [1, 1])), np.array(lose([4], [0]))]).astype(np.uint8)
+    bad[1, -1] = k + m + 3
+    bsrc = np.where(bad < k + m, bad, 0).astype(np.int16)
+    brecv = synth.assemble_received(data[:2], p_or[:2], bsrc)
+    b, rr, st = gpu_decode(engine, k, m, bb, brecv, bad, inplace=True)
+    assert st.tolist() == [-3, -3]
+    np.testing.assert_array_equal(rr, bad)
+    np.testing.assert_array_equal(b, brecv)
 
 
 # ------------------------------------------------- gf_bsyn (compiled (32, 4) decode, B/C)

@@ -1,7 +1,7 @@
 """ISA guard for the counted-vmcnt kernels (CPU only: hipcc cross-compiles gfx950).
 
 gf_stream_kernel / gf_ring_kernel (quic_amd/csrc/gf_stream.hip), gf_bsyn_kernel (gf_bsyn.hip)
-and gf_dcol_kernel (gf_dcol.hip) keep their own count of the VMEM instructions they issued and wait with `s_waitcnt vmcnt(N)` for
+gf_psyn_kernel (gf_psyn.hip) and gf_dcol_kernel (gf_dcol.hip) keep their own count of the VMEM instructions they issued and wait with `s_waitcnt vmcnt(N)` for
 exactly the pieces a block needs.  That is only sound if the compiler emits no VMEM
 instruction outside the count (a global_load of a uniform byte, a register spill, say) and
 inserts no vmcnt wait of its own (which would drain the pipeline).  This test compiles the
@@ -19,7 +19,7 @@ COUNTED = {"global_load_lds_dwordx4", "buffer_load_dwordx4", "buffer_store_dword
 DMA = ("global_load_lds_dwordx4", "buffer_load_dwordx4")   # the latter only as `... lds`
 
 
-@pytest.fixture(scope="module", params=["gf_stream", "gf_bsyn", "gf_dcol"])
+@pytest.fixture(scope="module", params=["gf_stream", "gf_bsyn", "gf_psyn", "gf_dcol"])
 def stream_isa(tmp_path_factory, request):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
@@ -38,7 +38,8 @@ def stream_isa(tmp_path_factory, request):
         out = str(tmp_path_factory.mktemp("isa") / f"{name}.s")
         subprocess.run(["python3", os.path.join(ROOT, "tools", "gen_cauchy_const.py")],
                        check=True, capture_output=True)
-        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17",
+        extra = ["-mllvm", "-simplifycfg-sink-common=false"] if name == "gf_psyn" else []
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", *extra,
                         "-mllvm", "-structurizecfg-skip-uniform-regions=true", "-DQFEC_BUILD",
                         "-I", os.path.join(ROOT, "build", "gen"), "-I", csrc,
                         "--cuda-device-only", "-S", "-o", out, src],

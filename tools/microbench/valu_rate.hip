@@ -22,6 +22,9 @@
 //             (v_bitop3 0x78 with the mask in an SGPR): 64 VALU per apply
 //   window    compile-time coefficient chosen by a 16-way uniform switch, windowed form
 //             (win_apply, 8 VALU per apply on a window built once per block)
+//   gpridx    run-time coefficient in the windowed form: acc[r] ^= lo[a_r] ^ hi[b_r] with the
+//             per-row nibbles (a_r, b_r) of c * alpha^r from a table and the window read by
+//             uniform register indexing (s_set_gpr_idx_on + v_mov): no branches
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../quic_amd/csrc valu_rate.hip -o valu_rate
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -103,7 +106,7 @@ __device__ __forceinline__ uint32_t coef_word(const uint32_t* __restrict__ tab, 
     return tab[it & 4095];
 }
 
-// OP 0 nibble, 1 mask, 2 window(switch)
+// OP 0 nibble, 1 mask, 2 window(switch), 3 gpridx
 template <int OP, int WPS>
 __global__ __launch_bounds__(256, WPS) void apply_kernel(const uint32_t* __restrict__ tab,
                                                          uint32_t* out, Stamp* st, uint32_t seed,
@@ -150,6 +153,22 @@ __global__ __launch_bounds__(256, WPS) void apply_kernel(const uint32_t* __restr
 #pragma unroll
                     for (int r = 0; r < 8; ++r)
                         acc[j][r] = __builtin_amdgcn_bitop3_b32(acc[j][r], W[bt + r], mk, 0x78);
+                }
+            }
+        } else if constexpr (OP == 3) {
+            // two plain local arrays (a struct would be left in scratch memory; plain arrays
+            // are promoted to registers and indexed with s_set_gpr_idx)
+            uint32_t lo[16], hi[16];
+            win_group(in, lo);
+            win_group(in + 4, hi);
+#pragma unroll
+            for (int j = 0; j < NOUT; ++j) {
+                // 8 bytes per coefficient: (a_r | b_r << 4) for r = 0..7
+                const uint32_t n0 = tab[(it * 8 + 2 * j) & 4095], n1 = tab[(it * 8 + 2 * j + 1) & 4095];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const uint32_t nb = ((r < 4 ? n0 : n1) >> (8 * (r & 3))) & 0xFFu;
+                    acc[j][r] = xor3(acc[j][r], lo[nb & 15u], hi[nb >> 4]);
                 }
             }
         } else {
@@ -282,5 +301,6 @@ int main() {
     APPLIES(0, "nibble")
     APPLIES(1, "mask")
     APPLIES(2, "window")
+    APPLIES(3, "gpridx")
     return 0;
 }
