@@ -15,11 +15,14 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
             -DQFEC_BUILD -DQFEC_TABLES_PATH='"$(TABLES)"' -Wall -Wno-unused-function \
             -MMD -MP -I$(ROOT)build/gen -I$(CSRC)
 
-SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_stream.hip $(CSRC)/gf_bsyn.hip $(CSRC)/gf_psyn.hip $(CSRC)/gf_dcol.hip $(CSRC)/pp_null.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp $(CSRC)/fec_wire.cpp
+# config D kernel instantiations, one per object (each compiles for minutes; -j builds them
+# in parallel)
+DCOLK := e61 e63 e83 d62 d63 d82
+SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_stream.hip $(CSRC)/gf_bsyn.hip $(CSRC)/gf_psyn.hip $(CSRC)/gf_dcol.hip $(DCOLK:%=$(CSRC)/gf_dcol_%.hip) $(CSRC)/pp_null.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp $(CSRC)/fec_wire.cpp
 # the headers every object depends on; the rest (include/*.h, pp_null.h, ...) are tracked per
 # object by -MMD below, so a public-header edit rebuilds only the host files that include it
 HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(CSRC)/gf_bitslice.h
-OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/xor_dma.o $(ROOT)build/gf_stream.o $(ROOT)build/gf_bsyn.o $(ROOT)build/gf_psyn.o $(ROOT)build/gf_dcol.o $(ROOT)build/pp_null.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o $(ROOT)build/fec_wire.o
+OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/xor_dma.o $(ROOT)build/gf_stream.o $(ROOT)build/gf_bsyn.o $(ROOT)build/gf_psyn.o $(ROOT)build/gf_dcol.o $(DCOLK:%=$(ROOT)build/gf_dcol_%.o) $(ROOT)build/pp_null.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o $(ROOT)build/fec_wire.o
 
 # Build guard (tools/check_stubs.py): every kernel stub a host pass registers has device code
 # in the same object.  Run after each HIP compile (the object is deleted on a mismatch) and on
@@ -84,7 +87,12 @@ $(ROOT)build/gf_psyn.o: $(CSRC)/gf_psyn.hip $(HDRS) $(GEN)
 	$(HIPCC) $(HIPFLAGS) $(PSYNFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }
 
-$(ROOT)build/gf_dcol.o: $(CSRC)/gf_dcol.hip $(HDRS) $(GEN)
+$(ROOT)build/gf_dcol.o: $(CSRC)/gf_dcol.hip $(CSRC)/gf_dcol.h $(HDRS) $(GEN)
+	@mkdir -p $(ROOT)build
+	$(HIPCC) $(HIPFLAGS) $(SAVE_ASM) -c $< -o $@
+	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }
+
+$(ROOT)build/gf_dcol_%.o: $(CSRC)/gf_dcol_%.hip $(CSRC)/gf_dcol.h $(HDRS) $(GEN)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }

@@ -618,11 +618,11 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"dma", &t.dma, 0, 1},                 {"stream", &t.stream, 0, 1},
         {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
         {"const_enc", &t.const_enc, 0, 1},     {"stream_static", &t.stream_static, 0, 1},
-        {"dcol_grid", &t.dcol_grid, 0, 1 << 20},
+        {"dcol_grid", &t.dcol_grid, 0, 1 << 20}, {"dcol_depth", &t.dcol_depth, 6, 8},
         {"bsyn", &t.bsyn, 0, 1},               {"dcol", &t.dcol, 0, 1},
         {"dcol_cache", &t.dcol_cache, 0, 3},     {"stream_rc16", &t.stream_rc16, 0, 1},
         {"ring_nt", &t.ring_nt, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
-        {"psyn", &t.psyn, 0, 1},               {"psyn_depth", &t.psyn_depth, 5, 9},
+        {"psyn", &t.psyn, 0, 1},               {"psyn_depth", &t.psyn_depth, 5, 9}, {"psyn_pf", &t.psyn_pf, 0, 1},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -631,7 +631,8 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
     };
     for (const Opt& o : opts) {
         if (strcmp(o.n, name) != 0) continue;
-        if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))))
+        if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))) ||
+            (o.p == &t.dcol_depth && value == 7) || (o.p == &t.psyn_depth && !(value & 1)))
             return fail(-2, std::string("option value out of range: ") + name);
         *o.p = value;
         return 0;
@@ -646,9 +647,9 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
     const std::pair<const char*, int> opts[] = {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
-        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"dcol_grid", t.dcol_grid},
+        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"dcol_grid", t.dcol_grid}, {"dcol_depth", t.dcol_depth},
         {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol}, {"dcol_cache", t.dcol_cache}, {"stream_rc16", t.stream_rc16},
-        {"ring_nt", t.ring_nt}, {"psyn", t.psyn}, {"psyn_depth", t.psyn_depth},
+        {"ring_nt", t.ring_nt}, {"psyn", t.psyn}, {"psyn_depth", t.psyn_depth}, {"psyn_pf", t.psyn_pf},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb}, {"host_min_groups", t.host_min_groups},
         {"pp_hash", c->pp_hash},

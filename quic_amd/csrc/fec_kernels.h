@@ -36,9 +36,13 @@ struct Tune {
     int psyn = 1;             // QuicR presets with m >= 7 at 1352 B: compiled syndrome decode
                               //   gf_psyn (0: the run-time gf_stream decode)
     int psyn_depth = 7;       // gf_psyn: blocks in flight per wave (5, 7, 9)
+    int psyn_pf = 1;          // gf_psyn: block b + 1 read into registers while block b is
+                              //   combined (0: read when consumed, fewer VGPRs)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16
                               //   rows; 0: gf_apply)
     int dcol_grid = 0;        // gf_dcol: grid cap in workgroups (0: CUs x per-CU fit)
+    int dcol_depth = 6;       // gf_dcol: blocks in flight per wave (6, or 8 with the default
+                              //   cache policy)
     int dcol_cache = 2;       // gf_dcol cache policy: encode 0 / 1 cached loads and non-temporal
                               //   stores, 2 / 3 cached loads and stores; decode (stores
                               //   plain) non-temporal loads for 0 / 2, cached 1 / 3

@@ -126,6 +126,21 @@ constexpr uint8_t gf_alpha_pow(int r) {
     return v;
 }
 
+// o[r] = (c * alpha^r) applied to the block, r = 0..7, for a compile-time coefficient C
+// (the product itself, no accumulator: one v_bitop3 or v_xor per sub-row, or a copy)
+template <unsigned C>
+__device__ __forceinline__ void win_set(uint32_t (&o)[8], const Win& w) {
+    static_for<8>([&](auto rc) __attribute__((always_inline)) {
+        constexpr int r = decltype(rc)::value;
+        constexpr unsigned M = gf_mul((uint8_t)C, gf_alpha_pow(r));
+        constexpr unsigned a = M & 15u, b = M >> 4;
+        if constexpr (a && b) o[r] = w.lo[a] ^ w.hi[b];
+        else if constexpr (a) o[r] = w.lo[a];
+        else if constexpr (b) o[r] = w.hi[b];
+        else o[r] = 0;
+    });
+}
+
 // acc[r] ^= (c * alpha^r) applied to the block, r = 0..7, for a compile-time coefficient C
 template <unsigned C>
 __device__ __forceinline__ void win_apply(uint32_t (&acc)[8], const Win& w) {

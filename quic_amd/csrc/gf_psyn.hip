@@ -110,8 +110,10 @@ struct PsynShape {
 constexpr int kPsynWaves = 4;   // waves per workgroup (independent)
 
 // KC, MC: the compiled code (k, m); RC = min(k, m): recovered blocks at most; S: sub-row
-// bytes; D: blocks in flight per wave.
-template <int KC, int MC, int RC, int S, int D>
+// bytes; D: blocks in flight per wave; PF: block b + 1 is read from LDS into registers while
+// block b is combined (16 more VGPRs; without, each block is read when its turn comes and
+// the other waves of the SIMD cover the LDS latency).
+template <int KC, int MC, int RC, int S, int D, bool PF>
 __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
     const uint8_t* __restrict__ cenc, const uint8_t* __restrict__ slots,
@@ -121,6 +123,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
     constexpr int BUFB = SH::BUFB, NPC = SH::NPC, P1L = SH::P1L;
     constexpr int NB = D + 1;                 // the block being read + D in flight
     constexpr int WAITN = (D - 1) * NPC;      // younger than block b + 1 when it is awaited
+    constexpr int WAITNF = D * NPC;           // (no PF) younger than block b when it is awaited
     static_assert(WAITN <= 63 && D >= 2 && KC >= D, "pipeline depth");
     static_assert(KC <= 64 && MC <= 32 && RC <= 16 && RC <= KC && RC <= MC && BB % 8 == 0 &&
                       NB <= 32,
@@ -187,8 +190,10 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
 #pragma unroll 1
     for (int u = 0; u < D; ++u) issue_next();
     uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
-    psyn_wait_vmcnt<WAITN>();
-    read_block(0, lo0, hi0);
+    if constexpr (PF) {
+        psyn_wait_vmcnt<WAITN>();
+        read_block(0, lo0, hi0);
+    }
 
     int b = 0;        // stream index of the block in (lo0, hi0) / the current block
     int prev_n = -1;  // recovered blocks the previous group stored (-1: no previous group)
@@ -227,6 +232,24 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                 wv[t] = (o & 3) ? __builtin_amdgcn_alignbyte(hi[t], lo[t], o & 3) : lo[t];
             }
         };
+        // (no PF) consume block b: prefetch block b + D, wait for block b (positions 0 .. D - 1
+        // of a group were DMA'd before the previous group's stores), read and realign it
+        auto take = [&](uint32_t (&wv)[8]) __attribute__((always_inline)) {
+            issue_next();
+            if (prev_n >= 0 && p <= D - 1)
+                psyn_wait_stores<WAITNF, 8 * SPR>(prev_n);
+            else
+                psyn_wait_vmcnt<WAITNF>();
+            uint32_t lo[8], hi[8];
+            read_block(b, lo, hi);
+            ++b;
+            ++p;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int o = t * S;
+                wv[t] = (o & 3) ? __builtin_amdgcn_alignbyte(hi[t], lo[t], o & 3) : lo[t];
+            }
+        };
         // data row x (compile time): its block, if present, into every syndrome row
         auto row_step = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
                             uint32_t (&nhi)[8]) __attribute__((always_inline)) {
@@ -234,14 +257,15 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
             const uint32_t mw = x < 32 ? mlo : mhi;
             if ((mw >> (x & 31)) & 1u) {
                 uint32_t wv[8];
-                advance(lo, hi, nlo, nhi, wv);
+                if constexpr (PF) advance(lo, hi, nlo, nhi, wv);
+                else take(wv);
                 Win win;
                 win_build(wv, win);
                 static_for<MC>([&](auto yc) __attribute__((always_inline)) {
                     constexpr int y = decltype(yc)::value;
                     win_apply<cauchy_coef(MC, y, x)>(acc[y], win);
                 });
-            } else {
+            } else if constexpr (PF) {
                 // row x erased: the block waiting in (lo, hi) is the next present row's
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
@@ -262,7 +286,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
         });
         // the row loop alternates (lo0, hi0) / (lo1, hi1): after an odd KC the next block is
         // in (lo1, hi1); the extras (and the next group) take it from (lo0, hi0)
-        if constexpr (KC % 2 == 1) {
+        if constexpr (PF && KC % 2 == 1) {
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
                 lo0[t] = lo1[t];
@@ -277,11 +301,15 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
 #pragma unroll 1
         for (int e = 0; e < ne; ++e) {
             WZ v;
-            advance(lo0, hi0, lo1, hi1, v.W8);
+            if constexpr (PF) {
+                advance(lo0, hi0, lo1, hi1, v.W8);
 #pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                lo0[t] = lo1[t];
-                hi0[t] = hi1[t];
+                for (int t = 0; t < 8; ++t) {
+                    lo0[t] = lo1[t];
+                    hi0[t] = hi1[t];
+                }
+            } else {
+                take(v.W8);
             }
             const int row = (int)((psyn_cload_u32(tb, psyn::kERow + (e & ~3)) >> (8 * (e & 3))) & 0xFFu);
             if (row >= KC) {
@@ -331,35 +359,35 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                         }
                     });
             });
-            // ---- Gauss-Jordan replay: pivot p expanded once, T_i ^= g[p][i] T_p for every
-            // slot (g[p][p] = 1 ^ inverse pivot)
+            // ---- Gauss-Jordan replay: the pivot row T_p windowed once (gf_bitslice.h), then
+            // T_i ^= g[p][i] T_p for every slot, g[p][p] = 1 ^ inverse pivot.  Each product
+            // is a 256-way uniform branch tree to the windowed code of that coefficient, a
+            // compile-time constant there (at most 8 VALU), into a temporary that is then
+            // scattered to slot i: one copy of the tree, not RC
 #pragma unroll 1
             for (int pv = 0; pv < n; ++pv) {
-                WZ v;
+                uint32_t pw[8];
                 psyn_dispatch<0, RC - 1>(pv, [&](auto pc) __attribute__((always_inline)) {
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) v.W[r] = acc[decltype(pc)::value][r];
+                    for (int r = 0; r < 8; ++r) pw[r] = acc[decltype(pc)::value][r];
                 });
-                expand_wz(v);
+                Win win;
+                win_build(pw, win);
                 const int cb = psyn::kCoef + 16 * pv;
                 uint32_t cw[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) cw[q] = psyn_cload_u32(tb, cb + 4 * q);
-                // one copy of the run-time apply (into a temporary), scattered to slot i:
-                // RC unrolled applies would put ~RC x 2 KB of dispatch code in the loop
 #pragma unroll 1
                 for (int ii = 0; ii < n; ++ii) {
-                    const uint32_t cf = (cw[0] >> (8 * ii)) & 0xFFu;
-                    uint32_t tmp[8];
+                    // the window is opaque per product: folded, every leaf's result is
+                    // loop-invariant and would be hoisted into registers
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        tmp[r] = 0;
-                        // opaque zero: the dispatch cases must stay in the loop (folded, they
-                        // are loop-invariant and ~70 of them would be hoisted into registers)
-                        asm volatile("" : "+v"(tmp[r]));
-                    }
-                    apply_nibble<0>(tmp, cf & 15u, v);
-                    apply_nibble<4>(tmp, cf >> 4, v);
+                    for (int q = 1; q < 16; ++q) asm volatile("" : "+v"(win.lo[q]), "+v"(win.hi[q]));
+                    const int cf = (int)((cw[0] >> (8 * (ii & 3))) & 0xFFu);
+                    uint32_t tmp[8];
+                    psyn_dispatch<0, 255>(cf, [&](auto cc) __attribute__((always_inline)) {
+                        win_set<decltype(cc)::value>(tmp, win);
+                    });
                     psyn_dispatch<0, RC - 1>(ii, [&](auto ic) __attribute__((always_inline)) {
 #pragma unroll
                         for (int r = 0; r < 8; ++r) acc[decltype(ic)::value][r] ^= tmp[r];
@@ -413,11 +441,18 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
 // status codes :1287-1294), then Gauss-Jordan without pivoting on S[s][j] = C[y_s][e_j]
 // (received parity rows ascending), recording per pivot p the coefficient g[p][i] the kernel
 // applies to T_p for slot i, and the psyn:: table.  k <= 64, m <= 32, rmax <= 16.
+// Lane s holds row s of S in registers (16 bytes); a pivot row reaches the group's lanes by
+// four shuffles, and a row update is n GF(256) products through the LDS log / exp tables.
 constexpr int kPsynLanes = 16;
 
 __device__ __forceinline__ void psyn_wave_sync() {
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int psyn_byte(const uint32_t (&w)[4], int c) {
+    const uint32_t v = c < 4 ? w[0] : c < 8 ? w[1] : c < 12 ? w[2] : w[3];
+    return (int)((v >> (8 * (c & 3))) & 0xFFu);
 }
 
 __global__ __launch_bounds__(256) void decode_prep_psyn_kernel(
@@ -429,8 +464,7 @@ __global__ __launch_bounds__(256) void decode_prep_psyn_kernel(
     __shared__ uint8_t glog[256];
     constexpr int GPB = 256 / kPsynLanes;                       // groups per block
     __shared__ uint8_t lrows[GPB][64];
-    __shared__ uint8_t lmat[GPB][16][16];                       // S, row-major
-    __shared__ uint8_t llist[GPB][4][16];                       // recpos, y (array order), ys, era
+    __shared__ uint8_t llist[GPB][3][16];                       // recpos, y (array order), era
     __shared__ __attribute__((aligned(16))) uint8_t ltab[GPB][psyn::kBytes];
     extern __shared__ __attribute__((aligned(16))) uint8_t lcenc[];   // m x k
     for (int i = threadIdx.x; i < 512; i += blockDim.x) gexp[i] = c_gf_psyn.exp[i];
@@ -445,36 +479,44 @@ __global__ __launch_bounds__(256) void decode_prep_psyn_kernel(
     __syncthreads();
     const int gl = threadIdx.x / kPsynLanes, l = threadIdx.x % kPsynLanes;
     const int seg = (threadIdx.x & 63) / kPsynLanes;            // the group's 16 lanes in the wave
+    const int sbase = (threadIdx.x & 63) - l;                   // lane 0 of the group in the wave
     const bool live = gl < ng;
     const long long g = gfirst + gl;
     const uint8_t* rg = lrows[gl];
-    uint8_t (*M)[16] = lmat[gl];
     uint8_t* lrec = llist[gl][0];
     uint8_t* ly = llist[gl][1];
-    uint8_t* lys = llist[gl][2];
-    uint8_t* lera = llist[gl][3];
+    uint8_t* lera = llist[gl][2];
     uint8_t* T = ltab[gl];
-    auto mul = [&](int a, int b2) -> int { return (a && b2) ? gexp[glog[a] + glog[b2]] : 0; };
 
     // ---- bookkeeping: slot i = 16 q + l.  isrec: slot i holds a recovery block; first: slot
     // i holds the first copy of its data row; present: data row r was received
-    uint64_t isrec = 0, first = 0, present = 0;
+    uint64_t isrec = 0, isdat = 0, present = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int i = kPsynLanes * q + l;
         const int r = (live && i < k) ? rg[i] : 0;
         const bool rec = live && i < k && r >= k;
-        bool fst = live && i < k && r < k;
-        if (fst)
-            for (int j = 0; j < i; ++j)
-                if (rg[j] == r) { fst = false; break; }
-        if (fst) present |= 1ull << r;
-        const uint64_t b1 = __ballot(rec), b2 = __ballot(fst);
+        const bool dat = live && i < k && r < k;
+        if (dat) present |= 1ull << r;
+        const uint64_t b1 = __ballot(rec), b2 = __ballot(dat);
         isrec |= ((b1 >> (kPsynLanes * seg)) & 0xFFFFull) << (kPsynLanes * q);
-        first |= ((b2 >> (kPsynLanes * seg)) & 0xFFFFull) << (kPsynLanes * q);
+        isdat |= ((b2 >> (kPsynLanes * seg)) & 0xFFFFull) << (kPsynLanes * q);
     }
 #pragma unroll
     for (int o = 1; o < kPsynLanes; o <<= 1) present |= __shfl_xor(present, o, kPsynLanes);
+    uint64_t first = isdat;
+    if (__popcll(isdat) != __popcll(present)) {   // a repeated data row (rare): find firsts
+        first = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = kPsynLanes * q + l;
+            bool fst = (isdat >> i) & 1;
+            if (fst)
+                for (int j = 0; j < i; ++j)
+                    if (rg[j] == rg[i]) { fst = false; break; }
+            first |= ((__ballot(fst) >> (kPsynLanes * seg)) & 0xFFFFull) << (kPsynLanes * q);
+        }
+    }
     const int nrec = __popcll(isrec);
     const uint64_t kmask = k == 64 ? ~0ull : ((1ull << k) - 1);
     const uint64_t missing = ~present & kmask;
@@ -489,7 +531,7 @@ __global__ __launch_bounds__(256) void decode_prep_psyn_kernel(
         if (e) myera = __ffsll((long long)e) - 1;
     }
     const int myy = myrec >= 0 ? rg[myrec] - k : 0;
-    const bool badrow = l < nrec && l < 16 && myy >= m;
+    const bool badrow = l < nrec && myy >= m;
     const bool anybad = (__ballot(badrow) >> (kPsynLanes * seg)) & 0xFFFFull;
     int early = 1;
     if (nrec == 0) early = 0;                                               // :1287-1289
@@ -502,46 +544,69 @@ __global__ __launch_bounds__(256) void decode_prep_psyn_kernel(
         lera[l] = (uint8_t)myera;
     }
     psyn_wave_sync();
-    if (l < n) {   // sorted position of y_l (ties by array order)
-        int pos = 0;
-        for (int j = 0; j < n; ++j) pos += (ly[j] < myy) || (ly[j] == myy && j < l);
-        lys[pos] = (uint8_t)myy;
+    // ---- row s of S = C[ys_s][e_j] in lane s (s = the rank of y_l: sorted ascending, ties by
+    // array order), packed 4 bytes per dword
+    int mys = 0;
+    for (int j = 0; j < n; ++j) mys += (ly[j] < myy) || (ly[j] == myy && j < l);
+    uint32_t row[4] = {0u, 0u, 0u, 0u};
+    if (l < n) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)   // compile-time indices: row[] stays in registers
+            if (j < n) row[j >> 2] |= (uint32_t)lcenc[myy * k + lera[j]] << (8 * (j & 3));
     }
+    // lane l ends up holding row s = mys; the shuffles below address rows by s, so the lane
+    // holding row s is found through lsrc (lane of row s)
+    __shared__ uint8_t lsrc[GPB][16];
+    if (l < n) lsrc[gl][mys] = (uint8_t)l;
     psyn_wave_sync();
-    // ---- S[s][j] = C[ys_s][e_j]: lane l owns column l
-    for (int s = 0; s < n; ++s)
-        if (l < n) M[s][l] = lcenc[lys[s] * k + lera[l]];
-    psyn_wave_sync();
+    const int ok_n = n;
     // ---- Gauss-Jordan without pivoting (every leading minor of a Cauchy submatrix is
     // nonzero); a zero pivot means a repeated parity row: malformed, status -3
-    for (int p = 0; p < n; ++p) {
-        const int piv = M[p][p];
+    for (int p = 0; p < ok_n; ++p) {
+        const int src = sbase + lsrc[gl][p];
+        uint32_t prow[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) prow[q] = (uint32_t)__shfl((int)row[q], src, 64);
+        const int piv = psyn_byte(prow, p);
         if (piv == 0) {
             early = -3;
             n = 0;
             break;
         }
-        const int inv = gexp[255 - glog[piv]];
-        uint8_t fcol[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) fcol[i] = i < n ? M[i][p] : 0;
-        const int mpl = l < n ? M[p][l] : 0;
-        psyn_wave_sync();
-        if (l < n) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                if (i < n && i != p && fcol[i]) M[i][l] ^= (uint8_t)mul(mul(fcol[i], inv), mpl);
-            M[p][l] = (uint8_t)mul(mpl, inv);
-            // the coefficient the kernel applies to T_p (before this step) for slot l
-            T[psyn::kCoef + 16 * p + l] = (uint8_t)(l == p ? (1 ^ inv) : mul(fcol[l], inv));
+        const int linv = 255 - glog[piv];                       // log of the inverse pivot
+        const int inv = gexp[linv];
+        const bool me = mys == p;
+        const int f = psyn_byte(row, p);
+        // the coefficient the kernel applies to T_p (before this step) for slot mys
+        int lg = 0, gco = 0;
+        if (me) {
+            gco = 1 ^ inv;
+            lg = linv;                                          // new row p = inv * row p
+        } else if (f) {
+            lg = glog[f] + linv;                                // row ^= (f / piv) * row p
+            gco = gexp[lg];
         }
-        psyn_wave_sync();
+        if (lg >= 255) lg -= 255;                               // lg + log(x) < 512: gexp's range
+        if (l < ok_n) T[psyn::kCoef + 16 * p + mys] = (uint8_t)gco;
+        if (l < ok_n && (me || f)) {
+            uint32_t nrow[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                if (c < ok_n) {
+                    const int pc = psyn_byte(prow, c);
+                    const int prod = pc ? gexp[lg + glog[pc]] : 0;
+                    nrow[c >> 2] |= (uint32_t)prod << (8 * (c & 3));
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) row[q] = me ? nrow[q] : (row[q] ^ nrow[q]);
+        }
     }
     // ---- the table: a changed group streams its present rows ascending, then the extras in
     // slot order; an unchanged one streams its slots in order as no-op extras (row tag 255)
     if (n > 0) {
         const int np = __popcll(present);
-        const uint64_t extra = ~first & (k == 64 ? ~0ull : ((1ull << k) - 1));
+        const uint64_t extra = ~first & kmask;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int i = kPsynLanes * q + l;
@@ -560,13 +625,16 @@ __global__ __launch_bounds__(256) void decode_prep_psyn_kernel(
             *(uint32_t*)(T + psyn::kMask) = (uint32_t)present;
             *(uint32_t*)(T + psyn::kMask + 4) = (uint32_t)(present >> 32);
         }
-        if (l < n) T[psyn::kYs + l] = lys[l];
+        if (l < n) T[psyn::kYs + mys] = (uint8_t)myy;
     } else {
         for (int i = l; i < k; i += kPsynLanes) {
             T[psyn::kPerm + i] = (uint8_t)i;
             T[psyn::kERow + i] = 255;
         }
-        // mask stays zero: the staged table was cleared
+        if (l == 0) {                                            // mask: nothing present
+            *(uint32_t*)(T + psyn::kMask) = 0u;
+            *(uint32_t*)(T + psyn::kMask + 4) = 0u;
+        }
     }
     if (live) {
         const uint8_t* rgg = rows_in + g * k;
@@ -646,13 +714,14 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
     using SH = PsynShape<kPsynS>;
     const int D = t.psyn_depth;
     if (D != 5 && D != 7 && D != 9) return hipErrorInvalidValue;
+    const bool pf = t.psyn_pf != 0;
     const size_t lds = (size_t)kPsynWaves * (D + 1) * SH::BUFB;
     const long long want = (groups + kPsynWaves - 1) / kPsynWaves;
     note_kernel("gf_psyn_kernel<decode,preset>");
     // persistent grid: the workgroups the CUs hold at once (registers and LDS decide)
-#define QP_GO(KV, MV, DV)                                                                      \
+#define QP_GO(KV, MV, DV, PFV)                                                                 \
     do {                                                                                       \
-        auto kern = gf_psyn_kernel<KV, MV, (KV < MV ? KV : MV), kPsynS, DV>;                   \
+        auto kern = gf_psyn_kernel<KV, MV, (KV < MV ? KV : MV), kPsynS, DV, PFV>;              \
         long long cap = (long long)t.cus * resident_blocks(kern, kPsynWaves * 64, lds);        \
         if (t.stream_grid > 0) cap = t.stream_grid;   /* tests: many groups per wave */        \
         const unsigned grid = (unsigned)std::min<long long>(want, cap);                       \
@@ -662,19 +731,23 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
         qlaunch(kern, dim3(grid), dim3(kPsynWaves * 64), lds, st, in, out, tab, cenc, slots,   \
                 nout, groups, rmax, out_gstride);                                              \
     } while (0)
-#define QP_CODE(DV)                                      \
-    switch (k * 256 + m) {                               \
-        case 10 * 256 + 10: QP_GO(10, 10, DV); break;    \
-        case 10 * 256 + 15: QP_GO(10, 15, DV); break;    \
-        case 10 * 256 + 20: QP_GO(10, 20, DV); break;    \
-        default: QP_GO(15, 15, DV); break;               \
+#define QP_CODE2(DV, PFV)                                     \
+    switch (k * 256 + m) {                                    \
+        case 10 * 256 + 10: QP_GO(10, 10, DV, PFV); break;    \
+        case 10 * 256 + 15: QP_GO(10, 15, DV, PFV); break;    \
+        case 10 * 256 + 20: QP_GO(10, 20, DV, PFV); break;    \
+        default: QP_GO(15, 15, DV, PFV); break;               \
     }
+#define QP_CODE(DV)                \
+    if (pf) QP_CODE2(DV, true)     \
+    else QP_CODE2(DV, false)
     switch (D) {
         case 5: QP_CODE(5); break;
         case 7: QP_CODE(7); break;
         default: QP_CODE(9); break;
     }
 #undef QP_CODE
+#undef QP_CODE2
 #undef QP_GO
     return hipGetLastError();
 }
