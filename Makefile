@@ -17,7 +17,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
 
 # config D kernel instantiations, one per object (each compiles for minutes; -j builds them
 # in parallel)
-DCOLK := e61 e63 e83 d62 d63 d82
+DCOLK := e61 e63 e83 d62 d63 d82 h43
 SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_stream.hip $(CSRC)/gf_bsyn.hip $(CSRC)/gf_psyn.hip $(CSRC)/gf_dcol.hip $(DCOLK:%=$(CSRC)/gf_dcol_%.hip) $(CSRC)/pp_null.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp $(CSRC)/fec_wire.cpp
 # the headers every object depends on; the rest (include/*.h, pp_null.h, ...) are tracked per
 # object by -MMD below, so a public-header edit rebuilds only the host files that include it

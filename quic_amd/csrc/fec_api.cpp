@@ -618,7 +618,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"dma", &t.dma, 0, 1},                 {"stream", &t.stream, 0, 1},
         {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
         {"const_enc", &t.const_enc, 0, 1},     {"stream_static", &t.stream_static, 0, 1},
-        {"dcol_grid", &t.dcol_grid, 0, 1 << 20}, {"dcol_depth", &t.dcol_depth, 6, 8},
+        {"dcol_grid", &t.dcol_grid, 0, 1 << 20}, {"dcol_depth", &t.dcol_depth, 6, 8}, {"dcol_rows", &t.dcol_rows, 8, 16},
         {"bsyn", &t.bsyn, 0, 1},               {"dcol", &t.dcol, 0, 1},
         {"dcol_cache", &t.dcol_cache, 0, 3},     {"stream_rc16", &t.stream_rc16, 0, 1},
         {"ring_nt", &t.ring_nt, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
@@ -632,7 +632,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
     for (const Opt& o : opts) {
         if (strcmp(o.n, name) != 0) continue;
         if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))) ||
-            (o.p == &t.dcol_depth && value == 7) || (o.p == &t.psyn_depth && !(value & 1)))
+            (o.p == &t.dcol_depth && value == 7) || (o.p == &t.dcol_rows && value != 8 && value != 16) || (o.p == &t.psyn_depth && !(value & 1)))
             return fail(-2, std::string("option value out of range: ") + name);
         *o.p = value;
         return 0;
@@ -647,7 +647,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
     const std::pair<const char*, int> opts[] = {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
-        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"dcol_grid", t.dcol_grid}, {"dcol_depth", t.dcol_depth},
+        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"dcol_grid", t.dcol_grid}, {"dcol_depth", t.dcol_depth}, {"dcol_rows", t.dcol_rows},
         {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol}, {"dcol_cache", t.dcol_cache}, {"stream_rc16", t.stream_rc16},
         {"ring_nt", t.ring_nt}, {"psyn", t.psyn}, {"psyn_depth", t.psyn_depth}, {"psyn_pf", t.psyn_pf},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},

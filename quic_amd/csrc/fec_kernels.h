@@ -43,6 +43,8 @@ struct Tune {
     int dcol_grid = 0;        // gf_dcol: grid cap in workgroups (0: CUs x per-CU fit)
     int dcol_depth = 6;       // gf_dcol: blocks in flight per wave (6, or 8 with the default
                               //   cache policy)
+    int dcol_rows = 16;       // gf_dcol encode: parity rows per wave (16, or 8: two waves per
+                              //   tile at four waves per SIMD)
     int dcol_cache = 2;       // gf_dcol cache policy: encode 0 / 1 cached loads and non-temporal
                               //   stores, 2 / 3 cached loads and stores; decode (stores
                               //   plain) non-temporal loads for 0 / 2, cached 1 / 3

@@ -896,16 +896,24 @@ D_KERNELS = {1: ("gf_dcol_kernel<encode,k128m16>", "gf_dcol_kernel<decode,k128m1
              0: ("gf_apply_kernel<encode", "gf_apply_kernel<decode")}
 
 
-@pytest.mark.parametrize("dcol", [1, 0])
+D_VARIANTS = [{"dcol": 1}, {"dcol": 1, "dcol_depth": 8}, {"dcol": 1, "dcol_rows": 8},
+              {"dcol": 0}]
+
+
+@pytest.mark.parametrize("opts", D_VARIANTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 @pytest.mark.parametrize("grid", [1, 3, 0])
 @pytest.mark.parametrize("k,m,r", [(128, 16, 8), (128, 16, 13), (40, 16, 16), (16, 6, 4)])
-def test_tile_many_groups_per_workgroup(tuned_engine, oracle, grid, k, m, r, dcol):
+def test_tile_many_groups_per_workgroup(tuned_engine, oracle, grid, k, m, r, opts):
     """Config D's kernels with the grid capped so one workgroup streams several groups back
     to back (the DMA prefetch crosses group / unit boundaries and the previous group's stores
     sit in the vmcnt count); every third group has no loss.  dcol = 1: gf_dcol (one wave
-    per column tile, units of (group, tile)); dcol = 0: the gf_apply fallback."""
+    per column tile, units of (group, tile)) with its ring depth and rows-per-wave variants
+    (dcol_rows = 8: half tiles, no register prefetch, 4 waves per SIMD; encode only);
+    dcol = 0: the gf_apply fallback."""
     engine = tuned_engine
-    engine.set_option("dcol", dcol)
+    for name, v in opts.items():
+        engine.set_option(name, v)
+    dcol = opts["dcol"]
     engine.set_option("dcol_grid", grid)
     bb, G = 9008, 7
     data = synth.group_data(4000 + k + m + grid, k, bb, G)
@@ -948,9 +956,10 @@ def check_decodes(engine, oracle, k, m, bb, recv, rows, dec_kernel):
     return s_or
 
 
-@pytest.mark.parametrize("dcol", [1, 0])
+@pytest.mark.parametrize("opts", [{"dcol": 1}, {"dcol": 1, "dcol_depth": 8}, {"dcol": 0}],
+                         ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 @pytest.mark.parametrize("grid", [1, 3, 0])
-def test_syndrome_decode_patterns(tuned_engine, oracle, grid, dcol):
+def test_syndrome_decode_patterns(tuned_engine, oracle, grid, opts):
     """Config D's decode (syndromes of the compiled (128, 16) code, then the r x r solve,
     gf_dcol_kernel; dcol = 0: the gf_apply fallback) on hand-built receive sets: no loss, 16 losses, single and scattered
     parity rows, more than 8 losses (two syndrome exchange rounds), a repeated data row (an
@@ -959,7 +968,9 @@ def test_syndrome_decode_patterns(tuned_engine, oracle, grid, dcol):
     k + m) are where the reference's result is not defined (its elimination runs on a
     singular bit matrix / reads past its Cauchy matrix): status -3, group left unchanged."""
     engine = tuned_engine
-    engine.set_option("dcol", dcol)
+    for name, v in opts.items():
+        engine.set_option(name, v)
+    dcol = opts["dcol"]
     engine.set_option("dcol_grid", grid)
     k, m, bb = 128, 16, 9008
     rng = np.random.default_rng(90 + grid)

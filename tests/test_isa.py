@@ -19,7 +19,9 @@ COUNTED = {"global_load_lds_dwordx4", "buffer_load_dwordx4", "buffer_store_dword
 DMA = ("global_load_lds_dwordx4", "buffer_load_dwordx4")   # the latter only as `... lds`
 
 
-DCOL = ["gf_dcol_e61", "gf_dcol_e63", "gf_dcol_e83", "gf_dcol_d62", "gf_dcol_d63", "gf_dcol_d82"]
+DCOL = ["gf_dcol_e61", "gf_dcol_e63", "gf_dcol_e83", "gf_dcol_d62", "gf_dcol_d63", "gf_dcol_d82",
+        "gf_dcol_h43"]
+WAVES4 = {"gf_dcol_h43"}
 
 
 @pytest.fixture(scope="module", params=["gf_stream", "gf_bsyn", "gf_psyn"] + DCOL)
@@ -56,6 +58,10 @@ def stream_isa(tmp_path_factory, request):
         bodies[m.group(1)] = text[m.end():end]
     assert len(bodies) >= (1 if name in DCOL else 2), "expected the kernel instantiations"
     assert not re.search(r"\.private_segment_fixed_size:\s+[1-9]", text), "register spills"
+    if name in WAVES4:
+        # the 8-row variant exists to run 4 waves per SIMD: at most 128 VGPRs
+        for v in re.findall(r"^\s+\.vgpr_count:\s+(\d+)", text, re.M):
+            assert int(v) <= 128, f"{name}: {v} VGPRs, 4 waves per SIMD need <= 128"
     return bodies
 
 
