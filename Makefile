@@ -68,6 +68,11 @@ SAVE_ASM := -save-temps=obj
 $(GEN): $(TABLES) $(ROOT)tools/gen_cauchy_const.py
 	python3 $(ROOT)tools/gen_cauchy_const.py
 
+# the 256-leaf jump table of the run-time windowed product (gf_winjump.h)
+WJGEN := $(ROOT)build/gen/win_jump.h
+$(WJGEN): $(ROOT)tools/gen_win_jump.py
+	python3 $(ROOT)tools/gen_win_jump.py
+
 $(ROOT)build/gf_stream.o: $(CSRC)/gf_stream.hip $(HDRS) $(GEN)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) $(SAVE_ASM) -c $< -o $@
@@ -82,7 +87,7 @@ $(ROOT)build/gf_bsyn.o: $(CSRC)/gf_bsyn.hip $(HDRS) $(GEN)
 # the branches' identical loads into one load with a computed index, which leaves the
 # arrays in scratch memory (VMEM outside the counted waits)
 PSYNFLAGS := -mllvm -simplifycfg-sink-common=false
-$(ROOT)build/gf_psyn.o: $(CSRC)/gf_psyn.hip $(HDRS) $(GEN)
+$(ROOT)build/gf_psyn.o: $(CSRC)/gf_psyn.hip $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) $(PSYNFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }

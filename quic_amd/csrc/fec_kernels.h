@@ -35,7 +35,9 @@ struct Tune {
     int bsyn_depth = 5;       // gf_bsyn: blocks in flight per wave (3..7)
     int psyn = 1;             // QuicR presets with m >= 7 at 1352 B: compiled syndrome decode
                               //   gf_psyn (0: the run-time gf_stream decode)
-    int psyn_depth = 7;       // gf_psyn: blocks in flight per wave (5, 7, 9)
+    int psyn_depth = 7;       // gf_psyn: blocks in flight per wave (5, 7)
+    int psyn_jump = 1;        // gf_psyn: solve products by an indirect jump into a leaf table
+                              //   (gf_winjump.h; 0: a 256-way tree of uniform branches)
     int psyn_pf = 1;          // gf_psyn: block b + 1 read into registers while block b is
                               //   combined (0: read when consumed, fewer VGPRs)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16

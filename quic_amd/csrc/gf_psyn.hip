@@ -44,6 +44,7 @@
 #include "fec_kernels.h"
 #include "gf256.h"
 #include "gf_bitslice.h"
+#include "gf_winjump.h"
 
 namespace qfec {
 
@@ -112,8 +113,10 @@ constexpr int kPsynWaves = 4;   // waves per workgroup (independent)
 // KC, MC: the compiled code (k, m); RC = min(k, m): recovered blocks at most; S: sub-row
 // bytes; D: blocks in flight per wave; PF: block b + 1 is read from LDS into registers while
 // block b is combined (16 more VGPRs; without, each block is read when its turn comes and
-// the other waves of the SIMD cover the LDS latency).
-template <int KC, int MC, int RC, int S, int D, bool PF>
+// the other waves of the SIMD cover the LDS latency).  JUMP: the solve's run-time products go
+// through one indirect jump into a table of 256 leaves (gf_winjump.h) instead of a 256-way
+// tree of uniform branches.
+template <int KC, int MC, int RC, int S, int D, bool PF, bool JUMP>
 __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
     const uint8_t* __restrict__ cenc, const uint8_t* __restrict__ slots,
@@ -385,9 +388,13 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                     for (int q = 1; q < 16; ++q) asm volatile("" : "+v"(win.lo[q]), "+v"(win.hi[q]));
                     const int cf = (int)((cw[0] >> (8 * (ii & 3))) & 0xFFu);
                     uint32_t tmp[8];
-                    psyn_dispatch<0, 255>(cf, [&](auto cc) __attribute__((always_inline)) {
-                        win_set<decltype(cc)::value>(tmp, win);
-                    });
+                    if constexpr (JUMP) {
+                        win_mul_rt(tmp, win, (uint32_t)cf);
+                    } else {
+                        psyn_dispatch<0, 255>(cf, [&](auto cc) __attribute__((always_inline)) {
+                            win_set<decltype(cc)::value>(tmp, win);
+                        });
+                    }
                     psyn_dispatch<0, RC - 1>(ii, [&](auto ic) __attribute__((always_inline)) {
 #pragma unroll
                         for (int r = 0; r < 8; ++r) acc[decltype(ic)::value][r] ^= tmp[r];
@@ -713,15 +720,15 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
         return hipErrorInvalidValue;
     using SH = PsynShape<kPsynS>;
     const int D = t.psyn_depth;
-    if (D != 5 && D != 7 && D != 9) return hipErrorInvalidValue;
-    const bool pf = t.psyn_pf != 0;
+    if (D != 5 && D != 7) return hipErrorInvalidValue;
+    const bool pf = t.psyn_pf != 0, jump = t.psyn_jump != 0;
     const size_t lds = (size_t)kPsynWaves * (D + 1) * SH::BUFB;
     const long long want = (groups + kPsynWaves - 1) / kPsynWaves;
     note_kernel("gf_psyn_kernel<decode,preset>");
     // persistent grid: the workgroups the CUs hold at once (registers and LDS decide)
-#define QP_GO(KV, MV, DV, PFV)                                                                 \
+#define QP_GO(KV, MV, DV, PFV, JV)                                                             \
     do {                                                                                       \
-        auto kern = gf_psyn_kernel<KV, MV, (KV < MV ? KV : MV), kPsynS, DV, PFV>;              \
+        auto kern = gf_psyn_kernel<KV, MV, (KV < MV ? KV : MV), kPsynS, DV, PFV, JV>;          \
         long long cap = (long long)t.cus * resident_blocks(kern, kPsynWaves * 64, lds);        \
         if (t.stream_grid > 0) cap = t.stream_grid;   /* tests: many groups per wave */        \
         const unsigned grid = (unsigned)std::min<long long>(want, cap);                       \
@@ -731,23 +738,24 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
         qlaunch(kern, dim3(grid), dim3(kPsynWaves * 64), lds, st, in, out, tab, cenc, slots,   \
                 nout, groups, rmax, out_gstride);                                              \
     } while (0)
-#define QP_CODE2(DV, PFV)                                     \
+#define QP_CODE3(DV, PFV, JV)                                 \
     switch (k * 256 + m) {                                    \
-        case 10 * 256 + 10: QP_GO(10, 10, DV, PFV); break;    \
-        case 10 * 256 + 15: QP_GO(10, 15, DV, PFV); break;    \
-        case 10 * 256 + 20: QP_GO(10, 20, DV, PFV); break;    \
-        default: QP_GO(15, 15, DV, PFV); break;               \
+        case 10 * 256 + 10: QP_GO(10, 10, DV, PFV, JV); break;\
+        case 10 * 256 + 15: QP_GO(10, 15, DV, PFV, JV); break;\
+        case 10 * 256 + 20: QP_GO(10, 20, DV, PFV, JV); break;\
+        default: QP_GO(15, 15, DV, PFV, JV); break;           \
     }
+#define QP_CODE2(DV, PFV)                \
+    if (jump) QP_CODE3(DV, PFV, true)    \
+    else QP_CODE3(DV, PFV, false)
 #define QP_CODE(DV)                \
     if (pf) QP_CODE2(DV, true)     \
     else QP_CODE2(DV, false)
-    switch (D) {
-        case 5: QP_CODE(5); break;
-        case 7: QP_CODE(7); break;
-        default: QP_CODE(9); break;
-    }
+    if (D == 5) QP_CODE(5)
+    else QP_CODE(7)
 #undef QP_CODE
 #undef QP_CODE2
+#undef QP_CODE3
 #undef QP_GO
     return hipGetLastError();
 }

@@ -1,0 +1,50 @@
+// gf_winjump.h — run-time GF(2^8) coefficient times a windowed block by one indirect jump.
+//
+// win_mul_rt(t, w, c): t[r] = (c * alpha^r) applied to the block whose window is w
+// (gf_bitslice.h Win), r = 0..7 — the same bytes as win_set<c>(t, w), for a wave-uniform c
+// known only at run time.  The table of 256 straight-line leaves (build/gen/win_jump.h,
+// tools/gen_win_jump.py) lies inline after the dispatch: leaf c starts QF_WIN_LEAF_BYTES * c
+// bytes past it, is 8 four-byte VOP1/VOP2 instructions and an s_branch past the table.  The
+// dispatch is s_getpc_b64, s_mul_i32, s_add_u32, s_add_u32, s_addc_u32, s_setpc_b64: against
+// the 256-way tree of uniform branches (8 levels of s_cmp + s_cbranch, ~16 scalar
+// instructions and 4 taken branches per product), six scalar instructions and two jumps.
+//
+// Every call site emits its own 9 KB table (code size), so the callers keep one call site
+// per kernel (a loop with `#pragma unroll 1` around it) and scatter the product from t.
+// The leaves only read the window and write t; the scratch SGPR pair s[88:89] and s90 are
+// declared clobbered.
+#pragma once
+#include "gf_bitslice.h"
+#include "win_jump.h"
+
+namespace qfec {
+
+__device__ __forceinline__ void win_mul_rt(uint32_t (&t)[8], const Win& w, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile(
+        "s_getpc_b64 s[88:89]\n\t"
+        "1:\n\t"
+        "s_mul_i32 s90, %[c], " QF_WIN_LEAF_BYTES_S "\n\t"
+        "s_add_u32 s90, s90, 2f-1b\n\t"
+        "s_add_u32 s88, s88, s90\n\t"
+        "s_addc_u32 s89, s89, 0\n\t"
+        "s_setpc_b64 s[88:89]\n\t"
+        "2:\n\t" QF_WIN_JUMP_LEAVES
+        : [t0] "=&v"(t[0]), [t1] "=&v"(t[1]), [t2] "=&v"(t[2]), [t3] "=&v"(t[3]),
+          [t4] "=&v"(t[4]), [t5] "=&v"(t[5]), [t6] "=&v"(t[6]), [t7] "=&v"(t[7])
+        : [c] "s"(c), [l1] "v"(w.lo[1]), [l2] "v"(w.lo[2]), [l3] "v"(w.lo[3]),
+          [l4] "v"(w.lo[4]), [l5] "v"(w.lo[5]), [l6] "v"(w.lo[6]), [l7] "v"(w.lo[7]),
+          [l8] "v"(w.lo[8]), [l9] "v"(w.lo[9]), [l10] "v"(w.lo[10]), [l11] "v"(w.lo[11]),
+          [l12] "v"(w.lo[12]), [l13] "v"(w.lo[13]), [l14] "v"(w.lo[14]), [l15] "v"(w.lo[15]),
+          [h1] "v"(w.hi[1]), [h2] "v"(w.hi[2]), [h3] "v"(w.hi[3]), [h4] "v"(w.hi[4]),
+          [h5] "v"(w.hi[5]), [h6] "v"(w.hi[6]), [h7] "v"(w.hi[7]), [h8] "v"(w.hi[8]),
+          [h9] "v"(w.hi[9]), [h10] "v"(w.hi[10]), [h11] "v"(w.hi[11]), [h12] "v"(w.hi[12]),
+          [h13] "v"(w.hi[13]), [h14] "v"(w.hi[14]), [h15] "v"(w.hi[15])
+        : "s88", "s89", "s90", "scc");
+#else
+    (void)w, (void)c;
+    for (int r = 0; r < 8; ++r) t[r] = 0;
+#endif
+}
+
+}  // namespace qfec

@@ -764,11 +764,12 @@ def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
         assert "gf_apply" not in fec.last_kernels()
 
 
+@pytest.mark.parametrize("jump", [1, 0])
 @pytest.mark.parametrize("pf", [1, 0])
-@pytest.mark.parametrize("depth", [5, 7, 9])
+@pytest.mark.parametrize("depth", [5, 7])
 @pytest.mark.parametrize("grid", [1, 2, 0])
 @pytest.mark.parametrize("k,m", sorted(PSYN))
-def test_psyn_decode_patterns(tuned_engine, oracle, k, m, depth, grid, pf):
+def test_psyn_decode_patterns(tuned_engine, oracle, k, m, depth, grid, pf, jump):
     """The preset decode (gf_psyn: syndromes of every parity row with the compiled code,
     Gauss-Jordan replayed on the data) on hand-built receive sets: no loss, 1 .. min(k, m)
     losses with first / scattered / last parity rows in any arrival order (blocks streamed
@@ -781,6 +782,7 @@ def test_psyn_decode_patterns(tuned_engine, oracle, k, m, depth, grid, pf):
     engine.set_option("stream_grid", grid)
     engine.set_option("psyn_depth", depth)
     engine.set_option("psyn_pf", pf)
+    engine.set_option("psyn_jump", jump)
     bb = 1352
     rmax = min(k, m)
     rng = np.random.default_rng(500 + 7 * k + m + depth + grid)

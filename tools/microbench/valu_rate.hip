@@ -25,13 +25,18 @@
 //   gpridx    run-time coefficient in the windowed form: acc[r] ^= lo[a_r] ^ hi[b_r] with the
 //             per-row nibbles (a_r, b_r) of c * alpha^r from a table and the window read by
 //             uniform register indexing (s_set_gpr_idx_on + v_mov): no branches
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../quic_amd/csrc valu_rate.hip -o valu_rate
+//   jump      run-time coefficient in the windowed form through one indirect jump into a
+//             table of 256 leaves (gf_winjump.h win_mul_rt), product into a temporary then
+//             XORed into the output: 16 VALU + 6 scalar instructions per apply
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../quic_amd/csrc -I../../build/gen
+//         valu_rate.hip -o valu_rate
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 
 #include "gf_bitslice.h"
+#include "gf_winjump.h"
 
 using namespace qfec;
 
@@ -106,7 +111,7 @@ __device__ __forceinline__ uint32_t coef_word(const uint32_t* __restrict__ tab, 
     return tab[it & 4095];
 }
 
-// OP 0 nibble, 1 mask, 2 window(switch), 3 gpridx
+// OP 0 nibble, 1 mask, 2 window(switch), 3 gpridx, 4 jump
 template <int OP, int WPS>
 __global__ __launch_bounds__(256, WPS) void apply_kernel(const uint32_t* __restrict__ tab,
                                                          uint32_t* out, Stamp* st, uint32_t seed,
@@ -169,6 +174,22 @@ __global__ __launch_bounds__(256, WPS) void apply_kernel(const uint32_t* __restr
                 for (int r = 0; r < 8; ++r) {
                     const uint32_t nb = ((r < 4 ? n0 : n1) >> (8 * (r & 3))) & 0xFFu;
                     acc[j][r] = xor3(acc[j][r], lo[nb & 15u], hi[nb >> 4]);
+                }
+            }
+        } else if constexpr (OP == 4) {
+            Win w;
+            win_build(in, w);
+#pragma unroll 1
+            for (int j = 0; j < NOUT; ++j) {
+                const uint32_t cf = (uint32_t)__builtin_amdgcn_readfirstlane((int)((cw >> (8 * j)) & 0xFFu));
+                uint32_t t[8];
+                win_mul_rt(t, w, cf);
+                // j is run-time (one call site): scatter through a 4-way uniform switch
+                switch (j) {
+#define QM_J(J) \
+    case J: _Pragma("unroll") for (int r = 0; r < 8; ++r) acc[J][r] ^= t[r]; break;
+                    QM_J(0) QM_J(1) QM_J(2) default: QM_J(3)
+#undef QM_J
                 }
             }
         } else {
@@ -302,5 +323,6 @@ int main() {
     APPLIES(1, "mask")
     APPLIES(2, "window")
     APPLIES(3, "gpridx")
+    APPLIES(4, "jump")
     return 0;
 }
