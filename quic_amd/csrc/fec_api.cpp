@@ -197,8 +197,15 @@ int ws_begin(qfec_ctx* c, hipStream_t st) {
     QF_HIP(hipStreamIsCapturing(st, &cs));
     if (cs != hipStreamCaptureStatusNone) return 0;
     if (c->ws_used && c->ws_stream != st) {
-        QF_HIP(hipEventRecord(c->ws_ev, c->ws_stream));
-        QF_HIP(hipStreamWaitEvent(st, c->ws_ev, 0));
+        // the previous stream is capturing into a graph: its decode has not been enqueued
+        // for execution, there is nothing to wait for (and an event recorded into a capture
+        // cannot be waited on from outside it)
+        hipStreamCaptureStatus ps = hipStreamCaptureStatusNone;
+        QF_HIP(hipStreamIsCapturing(c->ws_stream, &ps));
+        if (ps == hipStreamCaptureStatusNone) {
+            QF_HIP(hipEventRecord(c->ws_ev, c->ws_stream));
+            QF_HIP(hipStreamWaitEvent(st, c->ws_ev, 0));
+        }
     }
     return 0;
 }
@@ -623,7 +630,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"dcol_cache", &t.dcol_cache, 0, 3},     {"stream_rc16", &t.stream_rc16, 0, 1},
         {"ring_nt", &t.ring_nt, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
         {"psyn", &t.psyn, 0, 1},               {"psyn_depth", &t.psyn_depth, 5, 7}, {"psyn_pf", &t.psyn_pf, 0, 1},
-        {"psyn_jump", &t.psyn_jump, 0, 1},
+        {"psyn_jump", &t.psyn_jump, 0, 2},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -686,7 +693,9 @@ int qfec_ctx_create(int device, qfec_ctx** out) {
 void qfec_ctx_destroy(qfec_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->ws_used) (void)hipStreamSynchronize(c->ws_stream);   // the last use of the workspace
+    // the last use of the workspace may be on any stream the caller used (and may have
+    // destroyed since): wait for the whole device rather than for a stored stream handle
+    if (c->ws_used) (void)hipDeviceSynchronize();
     for (hipStream_t s : {c->stream, c->s_in, c->s_out})
         if (s) (void)hipStreamSynchronize(s);
     if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);

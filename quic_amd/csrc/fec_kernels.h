@@ -37,7 +37,8 @@ struct Tune {
                               //   gf_psyn (0: the run-time gf_stream decode)
     int psyn_depth = 7;       // gf_psyn: blocks in flight per wave (5, 7)
     int psyn_jump = 1;        // gf_psyn: solve products by an indirect jump into a leaf table
-                              //   (gf_winjump.h; 0: a 256-way tree of uniform branches)
+                              //   (gf_winjump.h; 1: 256 windowed leaves, 2: two nibble jumps
+                              //   per product; 0: a 256-way tree of uniform branches)
     int psyn_pf = 1;          // gf_psyn: block b + 1 read into registers while block b is
                               //   combined (0: read when consumed, fewer VGPRs)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16

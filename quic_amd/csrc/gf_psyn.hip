@@ -114,9 +114,11 @@ constexpr int kPsynWaves = 4;   // waves per workgroup (independent)
 // bytes; D: blocks in flight per wave; PF: block b + 1 is read from LDS into registers while
 // block b is combined (16 more VGPRs; without, each block is read when its turn comes and
 // the other waves of the SIMD cover the LDS latency).  JUMP: the solve's run-time products go
-// through one indirect jump into a table of 256 leaves (gf_winjump.h) instead of a 256-way
-// tree of uniform branches.
-template <int KC, int MC, int RC, int S, int D, bool PF, bool JUMP>
+// (1) through one indirect jump into a table of 256 leaves (gf_winjump.h win_mul_rt) into a
+// temporary scattered to its slot, or (2) through two nibble jumps straight into the slot's
+// accumulator (wz_mul_acc_rt, one call site per slot), instead of (0) a 256-way tree of
+// uniform branches.
+template <int KC, int MC, int RC, int S, int D, bool PF, int JUMP>
 __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
     const uint8_t* __restrict__ cenc, const uint8_t* __restrict__ slots,
@@ -374,12 +376,25 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
 #pragma unroll
                     for (int r = 0; r < 8; ++r) pw[r] = acc[decltype(pc)::value][r];
                 });
-                Win win;
-                win_build(pw, win);
                 const int cb = psyn::kCoef + 16 * pv;
                 uint32_t cw[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) cw[q] = psyn_cload_u32(tb, cb + 4 * q);
+                if constexpr (JUMP == 2) {
+                    // W/Z form, each slot's product by two nibble jumps straight into its
+                    // accumulator (one call site per slot, compile-time target)
+                    WZ v;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v.W[r] = pw[r];
+                    expand_wz(v);
+                    static_for<RC>([&](auto ic) __attribute__((always_inline)) {
+                        constexpr int i = decltype(ic)::value;
+                        if (i < n) wz_mul_acc_rt(acc[i], v, (cw[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+                    });
+                    continue;
+                }
+                Win win;
+                win_build(pw, win);
 #pragma unroll 1
                 for (int ii = 0; ii < n; ++ii) {
                     // the window is opaque per product: folded, every leaf's result is
@@ -388,7 +403,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                     for (int q = 1; q < 16; ++q) asm volatile("" : "+v"(win.lo[q]), "+v"(win.hi[q]));
                     const int cf = (int)((cw[0] >> (8 * (ii & 3))) & 0xFFu);
                     uint32_t tmp[8];
-                    if constexpr (JUMP) {
+                    if constexpr (JUMP == 1) {
                         win_mul_rt(tmp, win, (uint32_t)cf);
                     } else {
                         psyn_dispatch<0, 255>(cf, [&](auto cc) __attribute__((always_inline)) {
@@ -721,7 +736,8 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
     using SH = PsynShape<kPsynS>;
     const int D = t.psyn_depth;
     if (D != 5 && D != 7) return hipErrorInvalidValue;
-    const bool pf = t.psyn_pf != 0, jump = t.psyn_jump != 0;
+    const bool pf = t.psyn_pf != 0;
+    const int jump = t.psyn_jump;
     const size_t lds = (size_t)kPsynWaves * (D + 1) * SH::BUFB;
     const long long want = (groups + kPsynWaves - 1) / kPsynWaves;
     note_kernel("gf_psyn_kernel<decode,preset>");
@@ -746,8 +762,9 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
         default: QP_GO(15, 15, DV, PFV, JV); break;           \
     }
 #define QP_CODE2(DV, PFV)                \
-    if (jump) QP_CODE3(DV, PFV, true)    \
-    else QP_CODE3(DV, PFV, false)
+    if (jump == 2) QP_CODE3(DV, PFV, 2)  \
+    else if (jump) QP_CODE3(DV, PFV, 1)  \
+    else QP_CODE3(DV, PFV, 0)
 #define QP_CODE(DV)                \
     if (pf) QP_CODE2(DV, true)     \
     else QP_CODE2(DV, false)

@@ -48,3 +48,52 @@ __device__ __forceinline__ void win_mul_rt(uint32_t (&t)[8], const Win& w, uint3
 }
 
 }  // namespace qfec
+
+namespace qfec {
+
+// wz_mul_acc_rt(acc, v, c): acc[r] ^= (c * alpha^r) applied to the block whose W/Z expansion
+// is v (gf_bitslice.h expand_wz), r = 0..7 — apply_nibble<0>(acc, c & 15, v) then
+// apply_nibble<4>(acc, c >> 4, v) with each nibble's 16-way uniform branch tree replaced by
+// an indirect jump into a table of 16 leaves (QF_NIB_LEAVES_LO / _HI: 8 eight-byte VALU and
+// an s_branch each).  Its tables are 2.2 KB per call site, so the target accumulator can be
+// a compile-time choice (one call site per target).
+__device__ __forceinline__ void wz_mul_acc_rt(uint32_t (&acc)[8], const WZ& v, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile(
+        "s_getpc_b64 s[88:89]\n\t"
+        "1:\n\t"
+        "s_and_b32 s90, %[c], 15\n\t"
+        "s_mul_i32 s90, s90, " QF_NIB_LEAF_BYTES_S "\n\t"
+        "s_add_u32 s90, s90, 2f-1b\n\t"
+        "s_add_u32 s88, s88, s90\n\t"
+        "s_addc_u32 s89, s89, 0\n\t"
+        "s_setpc_b64 s[88:89]\n\t"
+        "2:\n\t" QF_NIB_LEAVES_LO
+        "5:\n\t"
+        "s_getpc_b64 s[88:89]\n\t"
+        "4:\n\t"
+        "s_bfe_u32 s90, %[c], 0x40004\n\t"
+        "s_mul_i32 s90, s90, " QF_NIB_LEAF_BYTES_S "\n\t"
+        "s_add_u32 s90, s90, 6f-4b\n\t"
+        "s_add_u32 s88, s88, s90\n\t"
+        "s_addc_u32 s89, s89, 0\n\t"
+        "s_setpc_b64 s[88:89]\n\t"
+        "6:\n\t" QF_NIB_LEAVES_HI
+        "7:\n\t"
+        : [a0] "+v"(acc[0]), [a1] "+v"(acc[1]), [a2] "+v"(acc[2]), [a3] "+v"(acc[3]),
+          [a4] "+v"(acc[4]), [a5] "+v"(acc[5]), [a6] "+v"(acc[6]), [a7] "+v"(acc[7])
+        : [c] "s"(c), [w0] "v"(v.W[0]), [w1] "v"(v.W[1]), [w2] "v"(v.W[2]), [w3] "v"(v.W[3]),
+          [w4] "v"(v.W[4]), [w5] "v"(v.W[5]), [w6] "v"(v.W[6]), [w7] "v"(v.W[7]),
+          [w8] "v"(v.W[8]), [w9] "v"(v.W[9]), [w10] "v"(v.W[10]), [w11] "v"(v.W[11]),
+          [w12] "v"(v.W[12]), [w13] "v"(v.W[13]), [w14] "v"(v.W[14]), [z0] "v"(v.Z[0]),
+          [z1] "v"(v.Z[1]), [z2] "v"(v.Z[2]), [z3] "v"(v.Z[3]), [z4] "v"(v.Z[4]),
+          [z5] "v"(v.Z[5]), [z6] "v"(v.Z[6]), [z7] "v"(v.Z[7]), [z8] "v"(v.Z[8]),
+          [z9] "v"(v.Z[9]), [z10] "v"(v.Z[10]), [z11] "v"(v.Z[11]), [z12] "v"(v.Z[12]),
+          [z13] "v"(v.Z[13])
+        : "s88", "s89", "s90", "scc");
+#else
+    (void)acc, (void)v, (void)c;
+#endif
+}
+
+}  // namespace qfec

@@ -28,6 +28,9 @@
 //   jump      run-time coefficient in the windowed form through one indirect jump into a
 //             table of 256 leaves (gf_winjump.h win_mul_rt), product into a temporary then
 //             XORed into the output: 16 VALU + 6 scalar instructions per apply
+//   nibjump   the W/Z nibble form with each nibble's dispatch an indirect jump into a table
+//             of 16 leaves (gf_winjump.h wz_mul_acc_rt), compile-time target: 16 VALU + 12
+//             scalar instructions per apply
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../quic_amd/csrc -I../../build/gen
 //         valu_rate.hip -o valu_rate
 #include <hip/hip_runtime.h>
@@ -111,7 +114,7 @@ __device__ __forceinline__ uint32_t coef_word(const uint32_t* __restrict__ tab, 
     return tab[it & 4095];
 }
 
-// OP 0 nibble, 1 mask, 2 window(switch), 3 gpridx, 4 jump
+// OP 0 nibble, 1 mask, 2 window(switch), 3 gpridx, 4 jump, 5 nibjump
 template <int OP, int WPS>
 __global__ __launch_bounds__(256, WPS) void apply_kernel(const uint32_t* __restrict__ tab,
                                                          uint32_t* out, Stamp* st, uint32_t seed,
@@ -192,6 +195,16 @@ __global__ __launch_bounds__(256, WPS) void apply_kernel(const uint32_t* __restr
 #undef QM_J
                 }
             }
+        } else if constexpr (OP == 5) {
+            WZ v;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v.W[t] = in[t];
+            expand_wz(v);
+            static_for<NOUT>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int j = decltype(jc)::value;
+                const uint32_t cf = (uint32_t)__builtin_amdgcn_readfirstlane((int)((cw >> (8 * j)) & 0xFFu));
+                wz_mul_acc_rt(acc[j], v, cf);
+            });
         } else {
             Win w;
             win_build(in, w);
@@ -324,5 +337,6 @@ int main() {
     APPLIES(2, "window")
     APPLIES(3, "gpridx")
     APPLIES(4, "jump")
+    APPLIES(5, "nibjump")
     return 0;
 }
