@@ -36,6 +36,7 @@ struct Tune {
     int psyn = 1;             // QuicR presets with m >= 7 at 1352 B: compiled syndrome decode
                               //   gf_psyn (0: the run-time gf_stream decode)
     int psyn_depth = 7;       // gf_psyn: blocks in flight per wave (5, 7)
+    int dec_nt = 0;           // gf_bsyn / gf_psyn: recovered blocks stored non-temporal
     int psyn_jump = 1;        // gf_psyn: solve products by an indirect jump into a leaf table
                               //   (gf_winjump.h; 1: 256 windowed leaves, 2: two nibble jumps
                               //   per product; 0: a 256-way tree of uniform branches)

@@ -95,7 +95,8 @@ constexpr int kBsynWaves = 4;   // waves per workgroup (independent)
 constexpr int kBsynRC = 4;      // recovered blocks per group (rmax <= 4)
 
 // KC, MC: the compiled code (k, m); S: sub-row bytes; D: blocks in flight per wave.
-template <int KC, int MC, int S, int D>
+// NTS: the recovered blocks are stored non-temporal (dec_nt option)
+template <int KC, int MC, int S, int D, bool NTS = false>
 __global__ __launch_bounds__(kBsynWaves * 64) void gf_bsyn_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
     const uint8_t* __restrict__ cenc, const uint8_t* __restrict__ slots,
@@ -322,12 +323,13 @@ __global__ __launch_bounds__(kBsynWaves * 64) void gf_bsyn_kernel(
             asm volatile("" : "+v"(vo), "+v"(vt));
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
-                __builtin_amdgcn_raw_buffer_store_b32(o[r], rs, vo, r * S, 0);
+                constexpr int SA = NTS ? 2 : 0;
+                __builtin_amdgcn_raw_buffer_store_b32(o[r], rs, vo, r * S, SA);
                 if (S & 2)
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o[r], rs, vt, r * S, 0);
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o[r], rs, vt, r * S, SA);
                 if (S & 1)
                     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(o[r] >> (8 * (S & 2))), rs, vt,
-                                                         r * S + (S & 2), 0);
+                                                         r * S + (S & 2), SA);
             }
         }
         asm volatile("" ::: "memory");
@@ -547,7 +549,7 @@ hipError_t launch_gf_bsyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
         return hipErrorInvalidValue;
     using SH = BsynShape<kBsynS>;
     const int D = t.bsyn_depth;
-    if (D < 3 || D > 7) return hipErrorInvalidValue;
+    if (D != 3 && D != 5 && D != 7) return hipErrorInvalidValue;
     const size_t lds = (size_t)kBsynWaves * (D + 1) * SH::BUFB;
     const int per_cu = std::max(1, std::min((int)((160 * 1024) / lds), 20 / kBsynWaves));
     const long long want = (groups + kBsynWaves - 1) / kBsynWaves;
@@ -559,13 +561,19 @@ hipError_t launch_gf_bsyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
         return hipErrorInvalidValue;
     note_kernel("gf_bsyn_kernel<decode,k32m4>");
 #define QB_GO(DV)                                                                             \
-    qlaunch((gf_bsyn_kernel<32, 4, kBsynS, DV>), dim3(grid), dim3(kBsynWaves * 64), lds, st, \
-            in, out, tab, cenc, slots, nout, groups, rmax, out_gstride)
+    do {                                                                                      \
+        if (t.dec_nt)                                                                         \
+            qlaunch((gf_bsyn_kernel<32, 4, kBsynS, DV, true>), dim3(grid),                    \
+                    dim3(kBsynWaves * 64), lds, st, in, out, tab, cenc, slots, nout, groups,  \
+                    rmax, out_gstride);                                                       \
+        else                                                                                  \
+            qlaunch((gf_bsyn_kernel<32, 4, kBsynS, DV, false>), dim3(grid),                   \
+                    dim3(kBsynWaves * 64), lds, st, in, out, tab, cenc, slots, nout, groups,  \
+                    rmax, out_gstride);                                                       \
+    } while (0)
     switch (D) {
         case 3: QB_GO(3); break;
-        case 4: QB_GO(4); break;
         case 5: QB_GO(5); break;
-        case 6: QB_GO(6); break;
         default: QB_GO(7); break;
     }
 #undef QB_GO

@@ -7,10 +7,10 @@
 // per block a lane builds the 2 x 15 XOR combinations of its column word's 4-sub-row
 // halves (22 VALU) and then every (row, sub-row) is one v_bitop3, 128 per block.
 //
-// Why this shape.  The D kernels are bound by VALU issue, and the chip's
-// VALU rate under load stays near 5.5e11 wave-instructions/s whatever the occupancy
-// (tools/microbench/valu_rate.hip: 4.5e11 at one wave per SIMD, 5.8e11 at eight).  So the
-// lever is the instruction count.  gf_tile split the 16 rows over two waves per column
+// Why this shape.  The D kernels are bound by VALU issue: the instruction
+// count per block and the cycles each VALU instruction costs at the kernel's occupancy
+// (tools/microbench/valu_rate.hip, profiles/r04/valu_rate.txt: 4.6 shader cycles per VALU per
+// SIMD at two waves per SIMD, 3.3 at four, 2.7 at eight).  gf_tile split the 16 rows over two waves per column
 // tile, which builds every block's window twice (2 x 97 VALU per tile and block against
 // ~157 here) and needs a workgroup barrier per block pair and, in the decode, an 80 KB LDS
 // exchange of the syndromes.  Here a wave holds all 128 accumulators (about 190 VGPRs,

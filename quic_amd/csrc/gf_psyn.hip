@@ -117,7 +117,7 @@ constexpr int kPsynWaves = 4;   // waves per workgroup (independent)
 // (1) through one indirect jump into a table of 256 leaves (gf_winjump.h win_mul_rt) into a
 // temporary scattered to its slot, or (2) through two nibble jumps straight into the slot's
 // accumulator (wz_mul_acc_rt, one call site per slot), instead of (0) a 256-way tree of
-// uniform branches.
+// uniform branches.  Bit 2 of JUMP (4): the recovered blocks are stored non-temporal (dec_nt).
 template <int KC, int MC, int RC, int S, int D, bool PF, int JUMP>
 __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
@@ -138,6 +138,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
     const int lane = threadIdx.x & 63;
     const int w = wave_id();
     uint8_t* ring = smem + (size_t)w * NB * BUFB;
+    constexpr int SA = (JUMP & 4) ? 2 : 0;    // recovered blocks stored non-temporal (dec_nt)
     const long long W = (long long)gridDim.x * kPsynWaves;
     const long long g0 = (long long)blockIdx.x * kPsynWaves + w;
     if (g0 >= groups) return;
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                 uint32_t cw[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) cw[q] = psyn_cload_u32(tb, cb + 4 * q);
-                if constexpr (JUMP == 2) {
+                if constexpr ((JUMP & 3) == 2) {
                     // W/Z form, each slot's product by two nibble jumps straight into its
                     // accumulator (one call site per slot, compile-time target)
                     WZ v;
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                     for (int q = 1; q < 16; ++q) asm volatile("" : "+v"(win.lo[q]), "+v"(win.hi[q]));
                     const int cf = (int)((cw[0] >> (8 * (ii & 3))) & 0xFFu);
                     uint32_t tmp[8];
-                    if constexpr (JUMP == 1) {
+                    if constexpr ((JUMP & 3) == 1) {
                         win_mul_rt(tmp, win, (uint32_t)cf);
                     } else {
                         psyn_dispatch<0, 255>(cf, [&](auto cc) __attribute__((always_inline)) {
@@ -442,12 +443,12 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                 asm volatile("" : "+v"(vo), "+v"(vt));
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
-                    __builtin_amdgcn_raw_buffer_store_b32(acc[j][r], rs, vo, r * S, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(acc[j][r], rs, vo, r * S, SA);
                     if (S & 2)
-                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)acc[j][r], rs, vt, r * S, 0);
+                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)acc[j][r], rs, vt, r * S, SA);
                     if (S & 1)
                         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(acc[j][r] >> (8 * (S & 2))),
-                                                             rs, vt, r * S + (S & 2), 0);
+                                                             rs, vt, r * S + (S & 2), SA);
                 }
             }
         });
@@ -761,10 +762,14 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
         case 10 * 256 + 20: QP_GO(10, 20, DV, PFV, JV); break;\
         default: QP_GO(15, 15, DV, PFV, JV); break;           \
     }
-#define QP_CODE2(DV, PFV)                \
-    if (jump == 2) QP_CODE3(DV, PFV, 2)  \
-    else if (jump) QP_CODE3(DV, PFV, 1)  \
-    else QP_CODE3(DV, PFV, 0)
+#define QP_CODE2(DV, PFV)                    \
+    if (jump == 2) {                         \
+        if (t.dec_nt) QP_CODE3(DV, PFV, 6)   \
+        else QP_CODE3(DV, PFV, 2)            \
+    } else if (jump) {                       \
+        if (t.dec_nt) QP_CODE3(DV, PFV, 5)   \
+        else QP_CODE3(DV, PFV, 1)            \
+    } else QP_CODE3(DV, PFV, 0)
 #define QP_CODE(DV)                \
     if (pf) QP_CODE2(DV, true)     \
     else QP_CODE2(DV, false)
