@@ -73,7 +73,7 @@ WJGEN := $(ROOT)build/gen/win_jump.h
 $(WJGEN): $(ROOT)tools/gen_win_jump.py
 	python3 $(ROOT)tools/gen_win_jump.py
 
-$(ROOT)build/gf_stream.o: $(CSRC)/gf_stream.hip $(HDRS) $(GEN)
+$(ROOT)build/gf_stream.o: $(CSRC)/gf_stream.hip $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }

@@ -36,6 +36,10 @@ struct Tune {
     int psyn = 1;             // QuicR presets with m >= 7 at 1352 B: compiled syndrome decode
                               //   gf_psyn (0: the run-time gf_stream decode)
     int psyn_depth = 7;       // gf_psyn: blocks in flight per wave (5, 7)
+    int stream_jump = 0;      // gf_stream decode (bb = 1352, <= 8 outputs per unit): run-time
+                              //   products by nibble jumps (gf_winjump.h) instead of trees
+    int psyn_ablate = 0;      // timing probe only (wrong results): gf_psyn without its stores
+                              //   (1), without its arithmetic (2), without both (3)
     int dec_nt = 0;           // gf_bsyn / gf_psyn: recovered blocks stored non-temporal
     int psyn_jump = 1;        // gf_psyn: solve products by an indirect jump into a leaf table
                               //   (gf_winjump.h; 1: 256 windowed leaves, 2: two nibble jumps

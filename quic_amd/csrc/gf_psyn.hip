@@ -118,6 +118,8 @@ constexpr int kPsynWaves = 4;   // waves per workgroup (independent)
 // temporary scattered to its slot, or (2) through two nibble jumps straight into the slot's
 // accumulator (wz_mul_acc_rt, one call site per slot), instead of (0) a 256-way tree of
 // uniform branches.  Bit 2 of JUMP (4): the recovered blocks are stored non-temporal (dec_nt).
+// Bits 3 and 4 (8, 16) are timing probes only (psyn_ablate; results wrong): no stores, no
+// arithmetic (each block XORed into one accumulator, no solve).
 template <int KC, int MC, int RC, int S, int D, bool PF, int JUMP>
 __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
@@ -265,12 +267,17 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                 uint32_t wv[8];
                 if constexpr (PF) advance(lo, hi, nlo, nhi, wv);
                 else take(wv);
-                Win win;
-                win_build(wv, win);
-                static_for<MC>([&](auto yc) __attribute__((always_inline)) {
-                    constexpr int y = decltype(yc)::value;
-                    win_apply<cauchy_coef(MC, y, x)>(acc[y], win);
-                });
+                if constexpr (JUMP & 16) {   // ablation probe: no arithmetic
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) acc[x % MC][r] ^= wv[r];
+                } else {
+                    Win win;
+                    win_build(wv, win);
+                    static_for<MC>([&](auto yc) __attribute__((always_inline)) {
+                        constexpr int y = decltype(yc)::value;
+                        win_apply<cauchy_coef(MC, y, x)>(acc[y], win);
+                    });
+                }
             } else if constexpr (PF) {
                 // row x erased: the block waiting in (lo, hi) is the next present row's
 #pragma unroll
@@ -348,7 +355,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                 }
             }
         }
-        if (n > 0) {
+        if (!(JUMP & 16) && n > 0) {
             // ---- T_s <- T_{y_s}: ascending, y_s >= s, so no source is overwritten early
             const uint32_t ys0 = psyn_cload_u32(tb, psyn::kYs), ys1 = psyn_cload_u32(tb, psyn::kYs + 4);
             const uint32_t ys2 = psyn_cload_u32(tb, psyn::kYs + 8), ys3 = psyn_cload_u32(tb, psyn::kYs + 12);
@@ -430,7 +437,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
         asm volatile("" ::: "memory");   // stores stay in issue order among the DMAs
         static_for<RC>([&](auto jc) __attribute__((always_inline)) {
             constexpr int j = decltype(jc)::value;
-            if (j < n) {
+            if (!(JUMP & 8) && j < n) {   // (JUMP & 8: ablation probe, no stores)
                 const int oslot = slots ? (int)((psyn_cload_u32(slots, (int)((g * rmax + j) & ~3LL)) >>
                                                  (8 * ((g * rmax + j) & 3))) & 0xFFu)
                                         : j;
@@ -773,7 +780,12 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
 #define QP_CODE(DV)                \
     if (pf) QP_CODE2(DV, true)     \
     else QP_CODE2(DV, false)
-    if (D == 5) QP_CODE(5)
+    if (t.psyn_ablate) {   // timing probes: depth 7, prefetch, nibble jumps, nt stores
+        if (D != 7 || !pf) return hipErrorInvalidValue;
+        if (t.psyn_ablate == 1) QP_CODE3(7, true, 14)
+        else if (t.psyn_ablate == 2) QP_CODE3(7, true, 22)
+        else QP_CODE3(7, true, 30)
+    } else if (D == 5) QP_CODE(5)
     else QP_CODE(7)
 #undef QP_CODE
 #undef QP_CODE2

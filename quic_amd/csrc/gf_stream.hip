@@ -34,6 +34,7 @@
 #include "cauchy_const.h"
 #include "fec_kernels.h"
 #include "gf_bitslice.h"
+#include "gf_winjump.h"
 
 namespace qfec {
 
@@ -97,7 +98,9 @@ constexpr int kMirror = 2;                 // mirrored slots: a block (<= 2 KiB 
 // neighbouring waves, so the re-reads hit L2).  Groups whose byte offset is 8 mod 16 (odd k
 // with bb = 8 mod 16: the reference's (5, 5) and (15, 15) presets at 1352-byte blocks) are
 // streamed from the 16-byte boundary below them, their blocks 8 bytes into the stream.
-template <int RC, int S, bool DECODE, int RCPT = (RC < 4 ? 4 : RC), int KC = 0>
+// NJ (decode): each run-time product is two nibble jumps straight into its output's
+// accumulator (gf_winjump.h wz_mul_acc_rt) instead of two 16-way uniform branch trees.
+template <int RC, int S, bool DECODE, int RCPT = (RC < 4 ? 4 : RC), int KC = 0, bool NJ = false>
 __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
@@ -313,8 +316,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                         for (int r = 0; r < 8; ++r) acc[0][r] ^= v.W[r];
                     } else if (j < n) {
                         const uint32_t cf = (cwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-                        apply_nibble<0>(acc[j], cf & 15u, v);
-                        apply_nibble<4>(acc[j], cf >> 4, v);
+                        if constexpr (NJ) {
+                            wz_mul_acc_rt(acc[j], v, cf);
+                        } else {
+                            apply_nibble<0>(acc[j], cf & 15u, v);
+                            apply_nibble<4>(acc[j], cf >> 4, v);
+                        }
                     }
                 }
             };
@@ -741,6 +748,17 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     qlaunch((gf_stream_kernel<RCV, SV, DEC, RCPV, KCV>), dim3(grid), dim3(threads), \
                        lds, st, in, out, coef, slots, nout, groups, k, m, rmax, coef_gstride,   \
                        out_gstride, R, s, nchunk)
+#define QS_GOJ(RCV, SV, DEC, RCPV, KCV)                                                       \
+    qlaunch((gf_stream_kernel<RCV, SV, DEC, RCPV, KCV, true>), dim3(grid), dim3(threads), \
+                       lds, st, in, out, coef, slots, nout, groups, k, m, rmax, coef_gstride,   \
+                       out_gstride, R, s, nchunk)
+#define QS_DECJ(SV)                                       \
+    switch (rc) {                                         \
+        case 2: QS_GOJ(2, SV, true, 4, 0); break;         \
+        case 4: QS_GOJ(4, SV, true, 4, 0); break;         \
+        case 8: QS_GOJ(8, SV, true, 8, 0); break;         \
+        default: return hipErrorInvalidValue;             \
+    }
 #define QS_DEC(SV)                                        \
     switch (rc) {                                         \
         case 2: QS_GO(2, SV, true, 4, 0); break;          \
@@ -787,7 +805,11 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     if (decode) {
         if (s == 169) {
             note_kernel("gf_stream_kernel<decode>");
-            QS_DEC(169)
+            if (t.stream_jump && rc <= 8) {
+                QS_DECJ(169)
+            } else {
+                QS_DEC(169)
+            }
         } else {
             note_kernel("gf_stream_kernel<decode,s>");
             QS_DEC(0)
@@ -831,6 +853,8 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     }
 #undef QS_ENC
 #undef QS_DEC
+#undef QS_DECJ
+#undef QS_GOJ
 #undef QS_GO
     return hipGetLastError();
 }

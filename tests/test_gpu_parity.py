@@ -461,6 +461,7 @@ OPTION_SETS = [
     {"stream_ring": 36}, {"host_chunk_mb": 1, "host_min_groups": 1}, {"const_enc": 0},
     {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 3}, {"dcol": 0}, {"dcol_cache": 0},
     {"dcol_cache": 1}, {"dcol_cache": 3}, {"stream_rc16": 1}, {"ring_nt": 0}, {"dec_nt": 1},
+    {"stream_jump": 1}, {"bsyn": 0, "stream_jump": 1},
 ]
 
 
@@ -732,8 +733,9 @@ PRESETS = [(5, 5), (10, 10), (10, 15), (10, 20), (15, 15), (250, 5)]   # quic_fe
 PSYN = {(10, 10), (10, 15), (10, 20), (15, 15)}   # m >= 7: gf_psyn's compiled syndrome decode
 
 
-@pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0, "stream_rc16": 1}],
-                         ids=["default", "grid1", "runtime_rc16"])
+@pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0, "stream_rc16": 1},
+                                  {"psyn": 0, "stream_jump": 1}],
+                         ids=["default", "grid1", "runtime_rc16", "runtime_jump"])
 @pytest.mark.parametrize("k,m", PRESETS)
 def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
     """QuicR's negotiated configurations with 1350-byte payloads (bb = 1352): odd k puts every
@@ -894,7 +896,7 @@ def test_bsyn_decode_patterns(tuned_engine, oracle, depth, grid):
 
 
 # ------------------------------------------------- gf_dcol (9008-byte blocks, config D)
-D_KERNELS = {1: ("gf_dcol_kernel<encode,k128m16>", "gf_dcol_kernel<decode,k128m16>"),
+D_KERNELS = {1: ("gf_dcol_kernel<encode,k128m16", "gf_dcol_kernel<decode,k128m16"),
              0: ("gf_apply_kernel<encode", "gf_apply_kernel<decode")}
 
 
