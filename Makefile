@@ -18,11 +18,13 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
 # config D kernel instantiations, one per object (each compiles for minutes; -j builds them
 # in parallel)
 DCOLK := e61 e63 e83 d62 d63 d82 h43
-SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_stream.hip $(CSRC)/gf_bsyn.hip $(CSRC)/gf_psyn.hip $(CSRC)/gf_dcol.hip $(DCOLK:%=$(CSRC)/gf_dcol_%.hip) $(CSRC)/pp_null.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp $(CSRC)/fec_wire.cpp
+# preset syndrome-decode instantiations, one object per code (gf_psyn.h)
+PSYNK := 1010 1015 1020 1515
+SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_stream.hip $(CSRC)/gf_bsyn.hip $(CSRC)/gf_psyn.hip $(PSYNK:%=$(CSRC)/gf_psyn_%.hip) $(CSRC)/gf_dcol.hip $(DCOLK:%=$(CSRC)/gf_dcol_%.hip) $(CSRC)/pp_null.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp $(CSRC)/fec_wire.cpp
 # the headers every object depends on; the rest (include/*.h, pp_null.h, ...) are tracked per
 # object by -MMD below, so a public-header edit rebuilds only the host files that include it
 HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(CSRC)/gf_bitslice.h
-OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/xor_dma.o $(ROOT)build/gf_stream.o $(ROOT)build/gf_bsyn.o $(ROOT)build/gf_psyn.o $(ROOT)build/gf_dcol.o $(DCOLK:%=$(ROOT)build/gf_dcol_%.o) $(ROOT)build/pp_null.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o $(ROOT)build/fec_wire.o
+OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/xor_dma.o $(ROOT)build/gf_stream.o $(ROOT)build/gf_bsyn.o $(ROOT)build/gf_psyn.o $(PSYNK:%=$(ROOT)build/gf_psyn_%.o) $(ROOT)build/gf_dcol.o $(DCOLK:%=$(ROOT)build/gf_dcol_%.o) $(ROOT)build/pp_null.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o $(ROOT)build/fec_wire.o
 
 # Build guard (tools/check_stubs.py): every kernel stub a host pass registers has device code
 # in the same object.  Run after each HIP compile (the object is deleted on a mismatch) and on
@@ -87,7 +89,12 @@ $(ROOT)build/gf_bsyn.o: $(CSRC)/gf_bsyn.hip $(HDRS) $(GEN)
 # the branches' identical loads into one load with a computed index, which leaves the
 # arrays in scratch memory (VMEM outside the counted waits)
 PSYNFLAGS := -mllvm -simplifycfg-sink-common=false
-$(ROOT)build/gf_psyn.o: $(CSRC)/gf_psyn.hip $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
+$(ROOT)build/gf_psyn.o: $(CSRC)/gf_psyn.hip $(CSRC)/gf_psyn.h $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
+	@mkdir -p $(ROOT)build
+	$(HIPCC) $(HIPFLAGS) $(PSYNFLAGS) $(SAVE_ASM) -c $< -o $@
+	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }
+
+$(ROOT)build/gf_psyn_%.o: $(CSRC)/gf_psyn_%.hip $(CSRC)/gf_psyn.h $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) $(PSYNFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }

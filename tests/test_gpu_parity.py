@@ -766,7 +766,7 @@ def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
         assert "gf_apply" not in fec.last_kernels()
 
 
-@pytest.mark.parametrize("jump", [1, 2, 0])
+@pytest.mark.parametrize("jump", [2, 0])
 @pytest.mark.parametrize("pf", [1, 0])
 @pytest.mark.parametrize("depth", [5, 7])
 @pytest.mark.parametrize("grid", [1, 2, 0])

@@ -14,7 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = "/opt/rocm/bin/hipcc"
-COUNTED = {"global_load_lds_dwordx4", "buffer_load_dwordx4", "buffer_store_dword",
+COUNTED = {"global_load_lds_dwordx4", "buffer_load_dwordx4", "buffer_store_dword", "buffer_store_dwordx2",
            "buffer_store_short", "buffer_store_byte"}
 DMA = ("global_load_lds_dwordx4", "buffer_load_dwordx4")   # the latter only as `... lds`
 
@@ -22,9 +22,10 @@ DMA = ("global_load_lds_dwordx4", "buffer_load_dwordx4")   # the latter only as 
 DCOL = ["gf_dcol_e61", "gf_dcol_e63", "gf_dcol_e83", "gf_dcol_d62", "gf_dcol_d63", "gf_dcol_d82",
         "gf_dcol_h43"]
 WAVES4 = {"gf_dcol_h43"}
+PSYN = ["gf_psyn_1010", "gf_psyn_1015", "gf_psyn_1020", "gf_psyn_1515"]
 
 
-@pytest.fixture(scope="module", params=["gf_stream", "gf_bsyn", "gf_psyn"] + DCOL)
+@pytest.fixture(scope="module", params=["gf_stream", "gf_bsyn"] + PSYN + DCOL)
 def stream_isa(tmp_path_factory, request):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
@@ -35,16 +36,17 @@ def stream_isa(tmp_path_factory, request):
     built = os.path.join(ROOT, "build", f"{name}-hip-amdgcn-amd-amdhsa-gfx950.s")
     csrc = os.path.join(ROOT, "quic_amd", "csrc")
     inputs = [src] + [os.path.join(csrc, h) for h in ("fec_kernels.h", "gf_bitslice.h", "gf256.h",
-                                                      "gf_dcol.h")]
-    inputs += [os.path.join(ROOT, "tools", "gen_cauchy_const.py")]
+                                                      "gf_dcol.h", "gf_psyn.h", "gf_winjump.h")]
+    inputs += [os.path.join(ROOT, "tools", f) for f in ("gen_cauchy_const.py", "gen_win_jump.py")]
     if os.path.exists(built) and all(os.path.getmtime(built) >= os.path.getmtime(f)
                                      for f in inputs):
         out = built
     else:
         out = str(tmp_path_factory.mktemp("isa") / f"{name}.s")
-        subprocess.run(["python3", os.path.join(ROOT, "tools", "gen_cauchy_const.py")],
-                       check=True, capture_output=True)
-        extra = ["-mllvm", "-simplifycfg-sink-common=false"] if name == "gf_psyn" else []
+        for gen in ("gen_cauchy_const.py", "gen_win_jump.py"):
+            subprocess.run(["python3", os.path.join(ROOT, "tools", gen)], check=True,
+                           capture_output=True)
+        extra = ["-mllvm", "-simplifycfg-sink-common=false"] if name.startswith("gf_psyn") else []
         subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", *extra,
                         "-mllvm", "-structurizecfg-skip-uniform-regions=true", "-DQFEC_BUILD",
                         "-I", os.path.join(ROOT, "build", "gen"), "-I", csrc,
