@@ -420,17 +420,10 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                 // The staging accesses are inline asm with explicit lgkmcnt waits: as C++ LDS
                 // accesses the compiler would first wait for every LDS-DMA in flight
                 // (vmcnt(0)), since it cannot tell the staging buffer from the ring.
-                const uint32_t sb = (uint32_t)(uintptr_t)stage;
-                if (ln < NW) {
-                    // sub-row t at byte t * S; the tail word's 3 bytes past the sub-row land on
-                    // the next sub-row's first bytes, which its (later) write overwrites
-                    const uint32_t qa = sb + 4u * (uint32_t)ln;
-#define QP_STW(R) \
-    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(qa), "v"(acc[j][R]), "n"((R) * S) : "memory")
-                    QP_STW(0); QP_STW(1); QP_STW(2); QP_STW(3);
-                    QP_STW(4); QP_STW(5); QP_STW(6); QP_STW(7);
-#undef QP_STW
-                }
+                const uint32_t sb =
+                    (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)stage;
+                static_assert(S == 169, "stage_block_169");
+                if (ln < NW) stage_block_169(sb, acc[j], ln);
                 static_assert(BB <= 3 * 512 && BB % 8 == 0, "three dwordx2 stores per block");
                 const uint32_t ra = sb + 8u * (uint32_t)ln;
                 uint64_t v0, v1, v2;

@@ -100,7 +100,12 @@ constexpr int kMirror = 2;                 // mirrored slots: a block (<= 2 KiB 
 // streamed from the 16-byte boundary below them, their blocks 8 bytes into the stream.
 // NJ (decode): each run-time product is two nibble jumps straight into its output's
 // accumulator (gf_winjump.h wz_mul_acc_rt) instead of two 16-way uniform branch trees.
-template <int RC, int S, bool DECODE, int RCPT = (RC < 4 ? 4 : RC), int KC = 0, bool NJ = false>
+// WIDE (compiled encode, S = 169): each output block is assembled in a per-wave LDS staging
+// buffer (inline-asm ds ops) and written with 3 dwordx2 stores of contiguous bytes instead
+// of 8 x (b32 + b8) sub-row stores (gf_psyn.h, wide_st option).
+constexpr int kStreamStage = 1360;
+template <int RC, int S, bool DECODE, int RCPT = (RC < 4 ? 4 : RC), int KC = 0, bool NJ = false,
+          bool WIDE = false>
 __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
@@ -123,6 +128,10 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const int w = wave_id();
     const int RB = R * 1024;
     uint8_t* ring = smem + (size_t)w * (R + kMirror) * 1024;
+    static_assert(!WIDE || (S == 169 && !DECODE), "wide stores: 1352-byte encode blocks");
+    const uint32_t stage =   // this wave's staging buffer (LDS address), after every wave's ring
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(
+            smem + (size_t)kStreamWaves * (R + kMirror) * 1024 + (size_t)w * kStreamStage);
     const long long W = (long long)gridDim.x * kStreamWaves;
     const long long g0 = (long long)blockIdx.x * kStreamWaves + w;   // the wave's first unit
     const long long NU = groups * nchunk;
@@ -352,6 +361,42 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
             uint32_t vo = lane < NWF ? 4u * (uint32_t)c : kSDrop;
             uint32_t vt = lane == NWF && NWF < NW ? 4u * (uint32_t)c : kSDrop;
             asm volatile("" : "+v"(vo), "+v"(vt));
+            if constexpr (WIDE) {
+                // 8 ds_write_b32 per lane at the sub-row offsets (the tail word's 3 extra bytes
+                // land on the next sub-row's start, overwritten by its later write; the last
+                // one's inside the staging pad), then 3 x 512 B read back and stored as
+                // contiguous 8-byte lanes (past the block: dropped by the buffer range; the
+                // reads past 1360 B touch the next wave's buffer or read zeros, unused)
+                const uint32_t ra = stage + 8u * (uint32_t)lane;
+#pragma unroll
+                for (int j = 0; j < RC; ++j) {
+                    const int jo = ch * RC + j;
+                    uint8_t* dst = out + g * out_gstride + (long long)jo * BB;
+                    const __amdgpu_buffer_rsrc_t rs =
+                        __builtin_amdgcn_make_buffer_rsrc(dst, 0, (unsigned)BB, 0x00020000);
+                    if (lane < NW) stage_block_169(stage, acc[j], lane);
+                    uint64_t v0, v1, v2;
+                    asm volatile("ds_read_b64 %0, %3\n\t"
+                                 "ds_read_b64 %1, %3 offset:512\n\t"
+                                 "ds_read_b64 %2, %3 offset:1024\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=&v"(v0), "=&v"(v1), "=&v"(v2)
+                                 : "v"(ra)
+                                 : "memory");
+                    const uint64_t vv[3] = {v0, v1, v2};
+#pragma unroll
+                    for (int h = 0; h < 3; ++h)
+                        __builtin_amdgcn_raw_buffer_store_b64(
+                            (__attribute__((ext_vector_type(2))) unsigned)(
+                                (unsigned)vv[h], (unsigned)(vv[h] >> 32)),
+                            rs, 512u * h + 8u * (uint32_t)lane, 0, SAUX);
+                    vm += 3;
+                }
+                asm volatile("" ::: "memory");
+                gbase += NP;
+                gslot0 = (gslot0 + NP) % R;
+                continue;
+            }
 #pragma unroll
             for (int j = 0; j < RC; ++j) {
                 if (j < n) {
@@ -723,7 +768,10 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     if (((uintptr_t)in & 15) != 0 || ((uintptr_t)slots & 3) != 0) return hipErrorInvalidValue;
     const int R = t.stream_ring;
     if (R < 4 || R > 36) return hipErrorInvalidValue;
-    const size_t lds = (size_t)kStreamWaves * (R + kMirror) * 1024;
+    const bool wide_enc = !decode && t.wide_st && t.const_enc && gf_stream_compiled(k, m, bb) &&
+                          bb == 1352 && (((uintptr_t)out | (uintptr_t)out_gstride) & 7) == 0 &&
+                          !(t.stream_static && k == 32 && m == 4);
+    const size_t lds = (size_t)kStreamWaves * ((R + kMirror) * 1024 + (wide_enc ? kStreamStage : 0));
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int per_cu = (int)((160 * 1024) / lds);
     // units: (group, chunk of rc outputs); encode chunks of 8 for m > 8 (m <= 8: one chunk
@@ -819,6 +867,24 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
             // BASELINE configs B/C and the QuicR presets at 1350-byte payloads: the code is
             // fixed at compile time (windowed form, every output in one unit)
             note_kernel("gf_stream_kernel<encode,compiled>");
+            if (wide_enc) {
+#define QS_GOW(RCV, RCPV, KCV)                                                                 \
+    qlaunch((gf_stream_kernel<RCV, 169, false, RCPV, KCV, false, true>), dim3(grid),           \
+            dim3(threads), lds, st, in, out, coef, slots, nout, groups, k, m, rmax,            \
+            coef_gstride, out_gstride, R, s, nchunk)
+                switch (k * 256 + m) {
+                    case 32 * 256 + 4: QS_GOW(4, 4, 32); break;
+                    case 5 * 256 + 5: QS_GOW(5, 8, 5); break;
+                    case 10 * 256 + 10: QS_GOW(10, 12, 10); break;
+                    case 10 * 256 + 15: QS_GOW(15, 16, 10); break;
+                    case 10 * 256 + 20: QS_GOW(20, 20, 10); break;
+                    case 15 * 256 + 15: QS_GOW(15, 16, 15); break;
+                    case 250 * 256 + 5: QS_GOW(5, 8, 250); break;
+                    default: return hipErrorInvalidValue;
+                }
+#undef QS_GOW
+                return hipGetLastError();
+            }
             switch (k * 256 + m) {
                 case 32 * 256 + 4: QS_GO(4, 169, false, 4, 32); break;
                 case 5 * 256 + 5: QS_GO(5, 169, false, 8, 5); break;

@@ -97,3 +97,41 @@ __device__ __forceinline__ void wz_mul_acc_rt(uint32_t (&acc)[8], const WZ& v, u
 }
 
 }  // namespace qfec
+
+namespace qfec {
+
+// stage_block_169(lds, w, lane): writes one 1352-byte block (8 sub-rows of 169 B) that the wave
+// holds bit-sliced (lane c < 43: column word c of each sub-row, bytes 169 t + 4 c ..) to LDS at
+// byte address `lds` (8-byte aligned) as its contiguous bytes, with ALIGNED ds_write_b32 only
+// (an unaligned one is replayed slowly and measured wrong).  Sub-row t starts (t * 169) & 3
+// bytes into a dword: lane c writes the dword at 169 t - a + 4 c, built from its own word and
+// lane c - 1's (DPP wave_shr:1); lane 0 takes the bytes before the sub-row (the previous
+// sub-row's last four, read from its lane 42 into an SGPR).  Sub-rows are written in order, so
+// where lane 42's dword runs into the next sub-row, that sub-row's lane 0 overwrites it with
+// the merged bytes.  Lanes >= 43 must be inactive (exec).
+__device__ __forceinline__ void stage_block_169(uint32_t lds, const uint32_t (&w)[8], int lane) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    constexpr int S = 169;
+    const uint32_t qa = lds + 4u * (uint32_t)lane;
+    uint32_t X = 0;   // previous sub-row's bytes 165..168 (wave-uniform)
+#define QF_STAGE_T(T)                                                                         \
+    {                                                                                         \
+        constexpr int a = ((T) * S) & 3;                                                      \
+        const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)X, (int)w[T], 0x138, \
+                                                                    0xF, 0xF, false);         \
+        const uint32_t v = a ? __builtin_amdgcn_alignbyte(w[T], prev, (4 - a) & 3) : w[T];    \
+        asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(qa), "v"(v), "n"((T) * S - a)      \
+                     : "memory");                                                             \
+        if ((T) < 7)                                                                          \
+            X = (uint32_t)__builtin_amdgcn_readlane(                                          \
+                (int)__builtin_amdgcn_alignbyte(w[T], prev, 1), 42);                          \
+    }
+    QF_STAGE_T(0) QF_STAGE_T(1) QF_STAGE_T(2) QF_STAGE_T(3)
+    QF_STAGE_T(4) QF_STAGE_T(5) QF_STAGE_T(6) QF_STAGE_T(7)
+#undef QF_STAGE_T
+#else
+    (void)lds, (void)w, (void)lane;
+#endif
+}
+
+}  // namespace qfec

@@ -461,7 +461,7 @@ OPTION_SETS = [
     {"stream_ring": 36}, {"host_chunk_mb": 1, "host_min_groups": 1}, {"const_enc": 0},
     {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 3}, {"dcol": 0}, {"dcol_cache": 0},
     {"dcol_cache": 1}, {"dcol_cache": 3}, {"stream_rc16": 1}, {"ring_nt": 0}, {"dec_nt": 1},
-    {"stream_jump": 1}, {"bsyn": 0, "stream_jump": 1},
+    {"stream_jump": 1}, {"bsyn": 0, "stream_jump": 1}, {"wide_st": 1},
 ]
 
 
@@ -734,8 +734,10 @@ PSYN = {(10, 10), (10, 15), (10, 20), (15, 15)}   # m >= 7: gf_psyn's compiled s
 
 
 @pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0, "stream_rc16": 1},
-                                  {"psyn": 0, "stream_jump": 1}],
-                         ids=["default", "grid1", "runtime_rc16", "runtime_jump"])
+                                  {"psyn": 0, "stream_jump": 1}, {"wide_st": 1},
+                                  {"wide_st": 1, "stream_grid": 1, "dec_nt": 1}],
+                         ids=["default", "grid1", "runtime_rc16", "runtime_jump", "wide",
+                              "wide_grid1_nt"])
 @pytest.mark.parametrize("k,m", PRESETS)
 def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
     """QuicR's negotiated configurations with 1350-byte payloads (bb = 1352): odd k puts every
@@ -766,12 +768,13 @@ def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
         assert "gf_apply" not in fec.last_kernels()
 
 
+@pytest.mark.parametrize("wide", [0, 1])
 @pytest.mark.parametrize("jump", [2, 0])
 @pytest.mark.parametrize("pf", [1, 0])
 @pytest.mark.parametrize("depth", [5, 7])
 @pytest.mark.parametrize("grid", [1, 2, 0])
 @pytest.mark.parametrize("k,m", sorted(PSYN))
-def test_psyn_decode_patterns(tuned_engine, oracle, k, m, depth, grid, pf, jump):
+def test_psyn_decode_patterns(tuned_engine, oracle, k, m, depth, grid, pf, jump, wide):
     """The preset decode (gf_psyn: syndromes of every parity row with the compiled code,
     Gauss-Jordan replayed on the data) on hand-built receive sets: no loss, 1 .. min(k, m)
     losses with first / scattered / last parity rows in any arrival order (blocks streamed
@@ -785,6 +788,7 @@ def test_psyn_decode_patterns(tuned_engine, oracle, k, m, depth, grid, pf, jump)
     engine.set_option("psyn_depth", depth)
     engine.set_option("psyn_pf", pf)
     engine.set_option("psyn_jump", jump)
+    engine.set_option("wide_st", wide)
     bb = 1352
     rmax = min(k, m)
     rng = np.random.default_rng(500 + 7 * k + m + depth + grid)
