@@ -103,28 +103,46 @@ namespace qfec {
 // stage_block_169(lds, w, lane): writes one 1352-byte block (8 sub-rows of 169 B) that the wave
 // holds bit-sliced (lane c < 43: column word c of each sub-row, bytes 169 t + 4 c ..) to LDS at
 // byte address `lds` (8-byte aligned) as its contiguous bytes, with ALIGNED ds_write_b32 only
-// (an unaligned one is replayed slowly and measured wrong).  Sub-row t starts (t * 169) & 3
+// (an unaligned one is replayed slowly and measured wrong).  Sub-row t starts a = (t * 169) & 3
 // bytes into a dword: lane c writes the dword at 169 t - a + 4 c, built from its own word and
-// lane c - 1's (DPP wave_shr:1); lane 0 takes the bytes before the sub-row (the previous
-// sub-row's last four, read from its lane 42 into an SGPR).  Sub-rows are written in order, so
-// where lane 42's dword runs into the next sub-row, that sub-row's lane 0 overwrites it with
-// the merged bytes.  Lanes >= 43 must be inactive (exec).
+// lane c - 1's (ds_bpermute; gfx950 has no DPP wave shift); lane 0 takes the bytes before the
+// sub-row (the previous sub-row's last four, read from its lane 42 into an SGPR).  Sub-rows are
+// written in order, so where lane 42's dword runs into the next sub-row, that sub-row's lane 0
+// overwrites it with the merged bytes.  Lanes >= 43 must be inactive (exec).  Inline asm with
+// its own lgkmcnt waits (as C++ LDS accesses the compiler would first wait for every LDS-DMA in
+// flight).
 __device__ __forceinline__ void stage_block_169(uint32_t lds, const uint32_t (&w)[8], int lane) {
 #if defined(__HIP_DEVICE_COMPILE__)
     constexpr int S = 169;
     const uint32_t qa = lds + 4u * (uint32_t)lane;
+    const uint32_t pa = 4u * (uint32_t)(lane - 1);   // lane 0's is replaced below
+    uint32_t p[8];   // lane c - 1's word of each sub-row
+    asm volatile(
+        "ds_bpermute_b32 %0, %8, %9\n\t"
+        "ds_bpermute_b32 %1, %8, %10\n\t"
+        "ds_bpermute_b32 %2, %8, %11\n\t"
+        "ds_bpermute_b32 %3, %8, %12\n\t"
+        "ds_bpermute_b32 %4, %8, %13\n\t"
+        "ds_bpermute_b32 %5, %8, %14\n\t"
+        "ds_bpermute_b32 %6, %8, %15\n\t"
+        "ds_bpermute_b32 %7, %8, %16\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(p[0]), "=&v"(p[1]), "=&v"(p[2]), "=&v"(p[3]), "=&v"(p[4]), "=&v"(p[5]),
+          "=&v"(p[6]), "=&v"(p[7])
+        : "v"(pa), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]),
+          "v"(w[7]));
     uint32_t X = 0;   // previous sub-row's bytes 165..168 (wave-uniform)
+    const bool l0 = lane == 0;
 #define QF_STAGE_T(T)                                                                         \
     {                                                                                         \
         constexpr int a = ((T) * S) & 3;                                                      \
-        const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)X, (int)w[T], 0x138, \
-                                                                    0xF, 0xF, false);         \
+        const uint32_t prev = l0 ? X : p[T];                                                  \
         const uint32_t v = a ? __builtin_amdgcn_alignbyte(w[T], prev, (4 - a) & 3) : w[T];    \
         asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(qa), "v"(v), "n"((T) * S - a)      \
                      : "memory");                                                             \
         if ((T) < 7)                                                                          \
             X = (uint32_t)__builtin_amdgcn_readlane(                                          \
-                (int)__builtin_amdgcn_alignbyte(w[T], prev, 1), 42);                          \
+                (int)__builtin_amdgcn_alignbyte(w[T], p[T], 1), 42);                          \
     }
     QF_STAGE_T(0) QF_STAGE_T(1) QF_STAGE_T(2) QF_STAGE_T(3)
     QF_STAGE_T(4) QF_STAGE_T(5) QF_STAGE_T(6) QF_STAGE_T(7)
