@@ -439,8 +439,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                 for (int h = 0; h < 3; ++h) {
                     const uint32_t o = 512u * h + 8u * (uint32_t)ln;   // past BB: dropped
                     __builtin_amdgcn_raw_buffer_store_b64(
-                        (__attribute__((ext_vector_type(2))) unsigned)((unsigned)vv[h],
-                                                                     (unsigned)(vv[h] >> 32)),
+                        qf_u32x2(vv[h]),
                         rs, o, 0, SA);
                 }
             } else if (!(JUMP & 8) && j < n) {   // (JUMP & 8: ablation probe, no stores)

@@ -387,8 +387,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
 #pragma unroll
                     for (int h = 0; h < 3; ++h)
                         __builtin_amdgcn_raw_buffer_store_b64(
-                            (__attribute__((ext_vector_type(2))) unsigned)(
-                                (unsigned)vv[h], (unsigned)(vv[h] >> 32)),
+                            qf_u32x2(vv[h]),
                             rs, 512u * h + 8u * (uint32_t)lane, 0, SAUX);
                     vm += 3;
                 }

@@ -100,6 +100,13 @@ __device__ __forceinline__ void wz_mul_acc_rt(uint32_t (&acc)[8], const WZ& v, u
 
 namespace qfec {
 
+// a 64-bit value as the two-dword vector the 8-byte buffer store takes (low dword first)
+typedef unsigned qf_u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ qf_u32x2_t qf_u32x2(uint64_t v) {
+    qf_u32x2_t r = {(unsigned)v, (unsigned)(v >> 32)};
+    return r;
+}
+
 // stage_block_169(lds, w, lane): writes one 1352-byte block (8 sub-rows of 169 B) that the wave
 // holds bit-sliced (lane c < 43: column word c of each sub-row, bytes 169 t + 4 c ..) to LDS at
 // byte address `lds` (8-byte aligned) as its contiguous bytes, with ALIGNED ds_write_b32 only
