@@ -42,7 +42,7 @@ struct Tune {
                               //   products by nibble jumps (gf_winjump.h) instead of trees
     int psyn_ablate = 0;      // timing probe only (wrong results): gf_psyn without its stores
                               //   (1), without its arithmetic (2), without both (3)
-    int dec_nt = 0;           // gf_bsyn / gf_psyn: recovered blocks stored non-temporal
+    int dec_nt = 1;           // gf_bsyn / gf_psyn: recovered blocks stored non-temporal
     int psyn_jump = 2;        // gf_psyn: solve products by two nibble jumps into leaf tables
                               //   (gf_winjump.h; 0: a 256-way tree of uniform branches; 1,
                               //   one 256-leaf jump + scatter, measured slower and removed)

@@ -112,7 +112,7 @@ __device__ __forceinline__ qf_u32x2_t qf_u32x2(uint64_t v) {
 // byte address `lds` (8-byte aligned) as its contiguous bytes, with ALIGNED ds_write_b32 only
 // (an unaligned one is replayed slowly and measured wrong).  Sub-row t starts a = (t * 169) & 3
 // bytes into a dword: lane c writes the dword at 169 t - a + 4 c, built from its own word and
-// lane c - 1's (ds_bpermute; gfx950 has no DPP wave shift); lane 0 takes the bytes before the
+// lane c - 1's (ds_bpermute); lane 0 takes the bytes before the
 // sub-row (the previous sub-row's last four, read from its lane 42 into an SGPR).  Sub-rows are
 // written in order, so where lane 42's dword runs into the next sub-row, that sub-row's lane 0
 // overwrites it with the merged bytes.  Lanes >= 43 must be inactive (exec).  Inline asm with

@@ -460,7 +460,7 @@ OPTION_SETS = [
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
     {"stream_ring": 36}, {"host_chunk_mb": 1, "host_min_groups": 1}, {"const_enc": 0},
     {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 3}, {"dcol": 0}, {"dcol_cache": 0},
-    {"dcol_cache": 1}, {"dcol_cache": 3}, {"stream_rc16": 1}, {"ring_nt": 0}, {"dec_nt": 1},
+    {"dcol_cache": 1}, {"dcol_cache": 3}, {"stream_rc16": 1}, {"ring_nt": 0}, {"dec_nt": 0},
     {"stream_jump": 1}, {"bsyn": 0, "stream_jump": 1}, {"wide_st": 1},
 ]
 
