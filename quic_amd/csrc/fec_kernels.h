@@ -35,7 +35,7 @@ struct Tune {
     int bsyn_depth = 5;       // gf_bsyn: blocks in flight per wave (3..7)
     int psyn = 1;             // QuicR presets with m >= 7 at 1352 B: compiled syndrome decode
                               //   gf_psyn (0: the run-time gf_stream decode)
-    int psyn_depth = 7;       // gf_psyn: blocks in flight per wave (5, 7)
+    int psyn_depth = 5;       // gf_psyn: blocks in flight per wave (5, 7)
     int wide_st = 0;          // gf_psyn: recovered blocks assembled in LDS and written with
                               //   8-byte stores of contiguous bytes (3 per block, not 16)
     int stream_jump = 0;      // gf_stream decode (bb = 1352, <= 8 outputs per unit): run-time
@@ -46,7 +46,7 @@ struct Tune {
     int psyn_jump = 2;        // gf_psyn: solve products by two nibble jumps into leaf tables
                               //   (gf_winjump.h; 0: a 256-way tree of uniform branches; 1,
                               //   one 256-leaf jump + scatter, measured slower and removed)
-    int psyn_pf = 1;          // gf_psyn: block b + 1 read into registers while block b is
+    int psyn_pf = 0;          // gf_psyn: block b + 1 read into registers while block b is
                               //   combined (0: read when consumed, fewer VGPRs)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16
                               //   rows; 0: gf_apply)
