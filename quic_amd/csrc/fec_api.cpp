@@ -632,7 +632,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"psyn", &t.psyn, 0, 1},               {"psyn_depth", &t.psyn_depth, 5, 7}, {"psyn_pf", &t.psyn_pf, 0, 1},
         {"psyn_jump", &t.psyn_jump, 0, 2},     {"dec_nt", &t.dec_nt, 0, 1},
         {"psyn_ablate", &t.psyn_ablate, 0, 3},  {"stream_jump", &t.stream_jump, 0, 1},
-        {"wide_st", &t.wide_st, 0, 1},
+        {"wide_st", &t.wide_st, 0, 1},         {"enc_split", &t.enc_split, 0, 1},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -659,7 +659,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
         {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"dcol_grid", t.dcol_grid}, {"dcol_depth", t.dcol_depth}, {"dcol_rows", t.dcol_rows},
         {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol}, {"dcol_cache", t.dcol_cache}, {"stream_rc16", t.stream_rc16},
-        {"ring_nt", t.ring_nt}, {"psyn", t.psyn}, {"psyn_depth", t.psyn_depth}, {"psyn_pf", t.psyn_pf}, {"psyn_jump", t.psyn_jump}, {"dec_nt", t.dec_nt}, {"psyn_ablate", t.psyn_ablate}, {"stream_jump", t.stream_jump}, {"wide_st", t.wide_st},
+        {"ring_nt", t.ring_nt}, {"psyn", t.psyn}, {"psyn_depth", t.psyn_depth}, {"psyn_pf", t.psyn_pf}, {"psyn_jump", t.psyn_jump}, {"dec_nt", t.dec_nt}, {"psyn_ablate", t.psyn_ablate}, {"stream_jump", t.stream_jump}, {"wide_st", t.wide_st}, {"enc_split", t.enc_split},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb}, {"host_min_groups", t.host_min_groups},
         {"pp_hash", c->pp_hash},

@@ -36,6 +36,7 @@ struct Tune {
     int psyn = 1;             // QuicR presets with m >= 7 at 1352 B: compiled syndrome decode
                               //   gf_psyn (0: the run-time gf_stream decode)
     int psyn_depth = 5;       // gf_psyn: blocks in flight per wave (5, 7)
+    int enc_split = 0;        // compiled preset encodes with m > 10 in two output chunks
     int wide_st = 0;          // gf_psyn: recovered blocks assembled in LDS and written with
                               //   8-byte stores of contiguous bytes (3 per block, not 16)
     int stream_jump = 0;      // gf_stream decode (bb = 1352, <= 8 outputs per unit): run-time

@@ -104,8 +104,11 @@ constexpr int kMirror = 2;                 // mirrored slots: a block (<= 2 KiB 
 // buffer (inline-asm ds ops) and written with 3 dwordx2 stores of contiguous bytes instead
 // of 8 x (b32 + b8) sub-row stores (gf_psyn.h, wide_st option).
 constexpr int kStreamStage = 1360;
+// MF (compiled encode): the code's m when the outputs are cut into two chunks of RC rows
+// (units (group, chunk) on neighbouring waves, the second re-reading the group through L2):
+// half the accumulators, so more waves per SIMD for m > 10.  0: one chunk, m = RC.
 template <int RC, int S, bool DECODE, int RCPT = (RC < 4 ? 4 : RC), int KC = 0, bool NJ = false,
-          bool WIDE = false>
+          bool WIDE = false, int MF = 0>
 __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
@@ -280,8 +283,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     cB[q] = cw[(k > 1 ? 1 : 0) * NCW + q];
                 }
             }
-            auto step = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
-                            uint32_t (&nhi)[8], uint32_t (&cc)[NCW]) {
+            auto step = [&](auto xc, auto chc, uint32_t (&lo)[8], uint32_t (&hi)[8],
+                            uint32_t (&nlo)[8], uint32_t (&nhi)[8], uint32_t (&cc)[NCW]) {
                 const int x = xc;
                 const uint32_t bn = next_pos(bpos);
                 if (x + 1 < k) {
@@ -302,9 +305,11 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     // is P0, all coefficients 1 (cauchy_256.cpp:1519-1523)
                     Win win;
                     win_build(v.W8, win);
+                    constexpr int MFC = MF ? MF : RC, J0 = decltype(chc)::value * RC;
                     static_for<RC>([&](auto jc) __attribute__((always_inline)) {
                         constexpr int j = decltype(jc)::value;
-                        win_apply<cauchy_coef(RC, j, decltype(xc)::value)>(acc[j], win);
+                        if constexpr (J0 + j < MFC)
+                            win_apply<cauchy_coef(MFC, J0 + j, decltype(xc)::value)>(acc[j], win);
                     });
                     return;
                 }
@@ -334,24 +339,47 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     }
                 }
             };
+            using I0 = std::integral_constant<int, 0>;
             if constexpr (KC > 0) {
-                static_for<KC>([&](auto xc) {
-                    // the accumulators are opaque at every block boundary: with all
-                    // coefficients constant, the XOR reassociation would otherwise flatten
-                    // the blocks' sums into one tree and keep every block's W/Z live
-                    // (~490 VGPRs)
+                auto blocks = [&](auto chc) {
+                    static_for<KC>([&](auto xc) {
+                        // the accumulators are opaque at every block boundary: with all
+                        // coefficients constant, the XOR reassociation would otherwise
+                        // flatten the blocks' sums into one tree and keep every block's W/Z
+                        // live (~490 VGPRs)
 #pragma unroll
-                    for (int j = 0; j < RC; ++j)
+                        for (int j = 0; j < RC; ++j)
 #pragma unroll
-                        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
-                    if constexpr (decltype(xc)::value % 2 == 0) step(xc, lo0, hi0, lo1, hi1, cA);
-                    else step(xc, lo1, hi1, lo0, hi0, cB);
-                });
+                            for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
+                        if constexpr (decltype(xc)::value % 2 == 0)
+                            step(xc, chc, lo0, hi0, lo1, hi1, cA);
+                        else
+                            step(xc, chc, lo1, hi1, lo0, hi0, cB);
+                    });
+                };
+                if constexpr (MF > RC) {
+                    static_assert(MF <= 2 * RC, "two chunks");
+                    if (ch == 0) blocks(I0{});
+                    else blocks(std::integral_constant<int, 1>{});
+                } else {
+                    // one chunk: the block loop inline, not through the lambda (the fully
+                    // unrolled 250-block loop of (250, 5) spills to scratch through it)
+                    static_for<KC>([&](auto xc) {
+#pragma unroll
+                        for (int j = 0; j < RC; ++j)
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
+                        if constexpr (decltype(xc)::value % 2 == 0)
+                            step(xc, I0{}, lo0, hi0, lo1, hi1, cA);
+                        else
+                            step(xc, I0{}, lo1, hi1, lo0, hi0, cB);
+                    });
+                }
             } else {
 #pragma unroll 1
                 for (int x = 0; x < k; x += 2) {
-                    step(x, lo0, hi0, lo1, hi1, cA);
-                    if (x + 1 < k) step(x + 1, lo1, hi1, lo0, hi0, cB);
+                    step(x, I0{}, lo0, hi0, lo1, hi1, cA);
+                    if (x + 1 < k) step(x + 1, I0{}, lo1, hi1, lo0, hi0, cB);
                 }
             }
             asm volatile("" ::: "memory");   // stores stay in issue order among the DMAs
@@ -757,6 +785,8 @@ bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& 
     return true;
 }
 
+static bool wide_enc_want(const Tune& t) { return t.wide_st != 0; }
+
 hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef,
                             const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
                             long long groups, int rc, int rmax, long long coef_gstride,
@@ -767,7 +797,9 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     if (((uintptr_t)in & 15) != 0 || ((uintptr_t)slots & 3) != 0) return hipErrorInvalidValue;
     const int R = t.stream_ring;
     if (R < 4 || R > 36) return hipErrorInvalidValue;
+    // (not (250, 5): its fully unrolled 250-block loop with the staging spills to scratch)
     const bool wide_enc = !decode && t.wide_st && t.const_enc && gf_stream_compiled(k, m, bb) &&
+                          k <= 32 &&
                           bb == 1352 && (((uintptr_t)out | (uintptr_t)out_gstride) & 7) == 0 &&
                           !(t.stream_static && k == 32 && m == 4);
     const size_t lds = (size_t)kStreamWaves * ((R + kMirror) * 1024 + (wide_enc ? kStreamStage : 0));
@@ -777,7 +809,11 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     // of exactly m outputs), decode chunks of rc for rmax > rc
     const int s = bb / 8;
     const bool compiled = !decode && t.const_enc && gf_stream_compiled(k, m, bb);
+    // compiled encodes of m > 10 in two chunks (enc_split option): (10,15) (15,15) as 8 + 7
+    // rows, (10,20) as 10 + 10
+    const bool split = compiled && t.enc_split && m > 10 && bb == 1352 && !wide_enc_want(t);
     const int nchunk = decode ? (rmax + rc - 1) / rc
+                       : split ? 2
                               : (compiled || m <= 8 || (rc == 16 && m <= 16)) ? 1 : (m + 7) / 8;
     const long long units = groups * nchunk;
     const long long want = (units + kStreamWaves - 1) / kStreamWaves;
@@ -866,6 +902,20 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
             // BASELINE configs B/C and the QuicR presets at 1350-byte payloads: the code is
             // fixed at compile time (windowed form, every output in one unit)
             note_kernel("gf_stream_kernel<encode,compiled>");
+            if (split) {
+#define QS_GOS(RCV, RCPV, KCV, MFV)                                                            \
+    qlaunch((gf_stream_kernel<RCV, 169, false, RCPV, KCV, false, false, MFV>), dim3(grid),     \
+            dim3(threads), lds, st, in, out, coef, slots, nout, groups, k, m, rmax,            \
+            coef_gstride, out_gstride, R, s, nchunk)
+                switch (k * 256 + m) {
+                    case 10 * 256 + 15: QS_GOS(8, 8, 10, 15); break;
+                    case 10 * 256 + 20: QS_GOS(10, 12, 10, 20); break;
+                    case 15 * 256 + 15: QS_GOS(8, 8, 15, 15); break;
+                    default: return hipErrorInvalidValue;
+                }
+#undef QS_GOS
+                return hipGetLastError();
+            }
             if (wide_enc) {
 #define QS_GOW(RCV, RCPV, KCV)                                                                 \
     qlaunch((gf_stream_kernel<RCV, 169, false, RCPV, KCV, false, true>), dim3(grid),           \
@@ -878,7 +928,6 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
                     case 10 * 256 + 15: QS_GOW(15, 16, 10); break;
                     case 10 * 256 + 20: QS_GOW(20, 20, 10); break;
                     case 15 * 256 + 15: QS_GOW(15, 16, 15); break;
-                    case 250 * 256 + 5: QS_GOW(5, 8, 250); break;
                     default: return hipErrorInvalidValue;
                 }
 #undef QS_GOW
