@@ -39,7 +39,7 @@ struct Tune {
     int enc_split = 0;        // compiled preset encodes with m > 10 in two output chunks
     int wide_st = 0;          // gf_psyn: recovered blocks assembled in LDS and written with
                               //   8-byte stores of contiguous bytes (3 per block, not 16)
-    int stream_jump = 0;      // gf_stream decode (bb = 1352, <= 8 outputs per unit): run-time
+    int stream_jump = 1;      // gf_stream decode (bb = 1352, <= 8 outputs per unit): run-time
                               //   products by nibble jumps (gf_winjump.h) instead of trees
     int psyn_ablate = 0;      // timing probe only (wrong results): gf_psyn without its stores
                               //   (1), without its arithmetic (2), without both (3)

@@ -461,7 +461,7 @@ OPTION_SETS = [
     {"stream_ring": 36}, {"host_chunk_mb": 1, "host_min_groups": 1}, {"const_enc": 0},
     {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 3}, {"dcol": 0}, {"dcol_cache": 0},
     {"dcol_cache": 1}, {"dcol_cache": 3}, {"stream_rc16": 1}, {"ring_nt": 0}, {"dec_nt": 0},
-    {"stream_jump": 1}, {"bsyn": 0, "stream_jump": 1}, {"wide_st": 1}, {"enc_split": 1},
+    {"stream_jump": 0}, {"bsyn": 0, "stream_jump": 1}, {"wide_st": 1}, {"enc_split": 1},
 ]
 
 
@@ -734,10 +734,10 @@ PSYN = {(10, 10), (10, 15), (10, 20), (15, 15)}   # m >= 7: gf_psyn's compiled s
 
 
 @pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0, "stream_rc16": 1},
-                                  {"psyn": 0, "stream_jump": 1}, {"wide_st": 1},
+                                  {"psyn": 0, "stream_jump": 0}, {"wide_st": 1},
                                   {"wide_st": 1, "stream_grid": 1, "dec_nt": 1},
                                   {"enc_split": 1}, {"enc_split": 1, "stream_grid": 1}],
-                         ids=["default", "grid1", "runtime_rc16", "runtime_jump", "wide",
+                         ids=["default", "grid1", "runtime_rc16", "runtime_trees", "wide",
                               "wide_grid1_nt", "split", "split_grid1"])
 @pytest.mark.parametrize("k,m", PRESETS)
 def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
