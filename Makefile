@@ -72,8 +72,10 @@ $(GEN): $(TABLES) $(ROOT)tools/gen_cauchy_const.py
 
 # the 256-leaf jump table of the run-time windowed product (gf_winjump.h)
 WJGEN := $(ROOT)build/gen/win_jump.h
+# (the generator rewrites the header only when its text changes; the touch marks it newer
+# than a changed generator)
 $(WJGEN): $(ROOT)tools/gen_win_jump.py
-	python3 $(ROOT)tools/gen_win_jump.py
+	python3 $(ROOT)tools/gen_win_jump.py && touch $@
 
 $(ROOT)build/gf_stream.o: $(CSRC)/gf_stream.hip $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
 	@mkdir -p $(ROOT)build

@@ -79,10 +79,9 @@ constexpr int kPsynStage = 1536;   // per-wave LDS staging buffer of the wide st
 // bytes; D: blocks in flight per wave; PF: block b + 1 is read from LDS into registers while
 // block b is combined (16 more VGPRs; without, each block is read when its turn comes and
 // the other waves of the SIMD cover the LDS latency).  JUMP: the solve's run-time products go
-// (1) through one indirect jump into a table of 256 leaves (gf_winjump.h win_mul_rt) into a
-// temporary scattered to its slot, or (2) through two nibble jumps straight into the slot's
-// accumulator (wz_mul_acc_rt, one call site per slot), instead of (0) a 256-way tree of
-// uniform branches.  Bit 2 of JUMP (4): the recovered blocks are stored non-temporal (dec_nt).
+// (2) through two nibble jumps straight into the slot's accumulator (gf_winjump.h
+// wz_mul_acc_rt, one call site per slot), or (0) through a 256-way tree of uniform branches
+// into a temporary scattered to its slot.  Bit 2 of JUMP (4): the recovered blocks are stored non-temporal (dec_nt).
 // Bits 3 and 4 (8, 16) are timing probes only (psyn_ablate; results wrong): no stores, no
 // arithmetic (each block XORed into one accumulator, no solve).
 template <int KC, int MC, int RC, int S, int D, bool PF, int JUMP>
@@ -383,13 +382,9 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                     for (int q = 1; q < 16; ++q) asm volatile("" : "+v"(win.lo[q]), "+v"(win.hi[q]));
                     const int cf = (int)((cw[0] >> (8 * (ii & 3))) & 0xFFu);
                     uint32_t tmp[8];
-                    if constexpr ((JUMP & 3) == 1) {
-                        win_mul_rt(tmp, win, (uint32_t)cf);
-                    } else {
-                        psyn_dispatch<0, 255>(cf, [&](auto cc) __attribute__((always_inline)) {
-                            win_set<decltype(cc)::value>(tmp, win);
-                        });
-                    }
+                    psyn_dispatch<0, 255>(cf, [&](auto cc) __attribute__((always_inline)) {
+                        win_set<decltype(cc)::value>(tmp, win);
+                    });
                     psyn_dispatch<0, RC - 1>(ii, [&](auto ic) __attribute__((always_inline)) {
 #pragma unroll
                         for (int r = 0; r < 8; ++r) acc[decltype(ic)::value][r] ^= tmp[r];

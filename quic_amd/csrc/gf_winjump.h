@@ -1,5 +1,7 @@
 // gf_winjump.h — run-time GF(2^8) coefficient times a windowed block by one indirect jump.
 //
+// (Not used by the product kernels: the microbenchmark's "jump" mode, measured slower than
+// the nibble jumps below with the scatter a caller needs; kept with its CPU table test.)
 // win_mul_rt(t, w, c): t[r] = (c * alpha^r) applied to the block whose window is w
 // (gf_bitslice.h Win), r = 0..7 — the same bytes as win_set<c>(t, w), for a wave-uniform c
 // known only at run time.  The table of 256 straight-line leaves (build/gen/win_jump.h,
