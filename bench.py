@@ -180,7 +180,8 @@ _DECODE_ARG = {"xor_dma_kernel": 2, "gf_apply_kernel": 1, "gf_ring_kernel": 3,
                "gf_stream_kernel": 2, "gf_dcol_kernel": 2}
 _DECODE_ONLY = ("decode_prep_kernel", "decode_prep_lane_kernel", "m1_prep_kernel",
                 "scatter_recovered_kernel", "rows_k1_kernel",
-                "gf_bsyn_kernel", "decode_prep_bsyn_kernel")
+                "gf_bsyn_kernel", "decode_prep_bsyn_kernel", "gf_psyn_kernel",
+                "decode_prep_psyn_kernel", "decode_prep_wide_kernel")
 _ENCODE_ONLY = ("replicate_kernel",)
 
 
@@ -707,9 +708,9 @@ def main():
     goodput = total_groups * k * payload / 2**30 / (elapsed / args.steps)
 
     phase = "encode" if enc_ms >= dec_ms else "decode"
-    traffic, traffic_src = pmc_traffic("B" if wname == "C" else wname, phase, G)
-    if wname == "P":
-        traffic, traffic_src = None, None
+    # PMC summaries: profiles/r*/pmc_<A|B|D>.json, pmc_P<k>_<m>.json for the presets (C: B's)
+    traffic, traffic_src = pmc_traffic(f"P{k}_{m}" if wname == "P" else "B" if wname == "C" else wname,
+                                       phase, G)
     if phase == "encode":
         dom = (kernels["encode"], enc_gbs, enc_bytes, enc_ms)
     else:

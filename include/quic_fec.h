@@ -243,6 +243,9 @@ QFEC_API const char *qfec_last_error(void);
 /* Names of the kernels this thread's last engine call launched, " + "-separated, e.g.
  * "decode_prep_lane_kernel + gf_stream_kernel<decode>" (bench.py reports it). */
 QFEC_API const char *qfec_last_kernels(void);
+/* Grids of the persistent kernels the last call on this thread launched, as space-separated
+ * "kernel=workgroups" entries (e.g. "gf_psyn_kernel=1024"); diagnostics and tests. */
+QFEC_API const char *qfec_last_grids(void);
 /* Measurement hook (bench.py's roofline timing).  While set, every engine call on this
  * thread records start_event (a hipEvent_t) at the start of its first kernel and
  * stop_event at the end of its last, through hipExtLaunchKernel, so the pair brackets the

@@ -86,6 +86,7 @@ SIGNATURES = {
                                            ctypes.POINTER(ctypes.c_int)]),
     "qfec_last_error": (ctypes.c_char_p, []),
     "qfec_last_kernels": (ctypes.c_char_p, []),
+    "qfec_last_grids": (ctypes.c_char_p, []),
     "qfec_set_timing_events": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "qfec_version": (ctypes.c_int, []),
 }

@@ -50,6 +50,7 @@ enum {
 
 thread_local std::string g_err;
 thread_local std::string g_kernels;   // kernels launched by this thread's last call
+thread_local std::string g_grids;     // "name=grid" of its persistent kernels
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -111,14 +112,8 @@ int stream_encode_rc(int k, int m, int bb, bool aligned, const qfec::Tune& t) {
 // Output chunk of a decode.  gf_stream decodes in units of 8 recovered blocks: a group with
 // at most 8 losses leaves its second unit empty, and empty units read nothing, while one unit
 // of 16 accumulators halves the occupancy for every group ((10, 10) at 5 losses: 0.615 ms
-// with 16, a whole group per unit).  t.stream_rc16 = 1 takes the single 16-block unit.
-int stream_decode_rc(int k, int m, int bb, int rmax, const uint8_t* d_blocks,
-                     const qfec::Tune& t) {
-    if (t.stream_rc16 && rmax > 8 && rmax <= 16 && ((uintptr_t)d_blocks & 15) == 0 &&
-        k + m <= 256 && bb % 8 == 0 && qfec::gf_stream_supported(k, m, bb, 16, true, t))
-        return 16;
-    return decode_rc(rmax);
-}
+// with 16 against 0.544 ms).
+int stream_decode_rc(int rmax) { return decode_rc(rmax); }
 
 struct DevBuf {
     void* p = nullptr;
@@ -154,10 +149,12 @@ struct qfec_ctx {
     qfec::Tune tune;
     int pp_hash = 0;   // packet protection's FNV chain: 0 six 22-bit limbs, 1 64-bit halves
     // The decode workspace (dcoef, dslots, dnout, dscratch) is one per context.  Calls may
-    // enqueue on any stream: a use on another stream than the previous use records ws_ev on
-    // that previous stream and waits for it, so uses of the workspace are ordered across
-    // streams (ws_begin / ws_end).
-    hipEvent_t ws_ev = nullptr;
+    // enqueue on any stream: every eager use records ws_ev after its kernels, and a use on
+    // another stream waits for it, so uses of the workspace are ordered across streams
+    // (ws_begin / ws_end).
+    hipEvent_t ws_ev = nullptr;      // on ws_helper, after the last eager use
+    hipEvent_t ws_tmp = nullptr;     // on the last eager use's stream
+    hipStream_t ws_helper = nullptr;
     hipStream_t ws_stream = nullptr;
     bool ws_used = false;
     // encode coefficient tables keyed by (k, m, rc): [nchunk][k][rcp]; decode cenc by (k, m)
@@ -179,40 +176,37 @@ namespace {
 
 int set_device(qfec_ctx* c) {
     g_kernels.clear();
+    g_grids.clear();
     qfec::launch_timing().first = true;
     QF_HIP(hipSetDevice(c->device));
     return 0;
 }
 
-// Order this call's use of the context's decode workspace after the previous use (which
-// may have been enqueued on another stream).  Not while `st` is capturing into a graph:
-// there the calls of one capture are ordered by the capturing stream itself.
-// The event is recorded only when a decode arrives on another stream than the previous
-// one, on that previous stream at that moment: it then follows every kernel already queued
-// there, the previous decode's included.  A decode on the same stream as the last needs no
-// event (stream order), so the common single-stream case queues no marker packet between
-// kernels (each one cost the command processor a few microseconds per call).
+// Order this call's use of the context's decode workspace after the previous eager use
+// (which may have been enqueued on another stream).  Not while `st` is capturing into a
+// graph: there the calls of one capture are ordered by the capturing stream itself.
+// ws_end records ws_ev on the stream of every eager use, right after its kernels, while that
+// stream is still eager; ws_begin waits on it when a use arrives on another stream, whatever
+// that previous stream is doing now (it may have started a capture since).  A use on the
+// same stream as the last needs no wait (stream order).
 int ws_begin(qfec_ctx* c, hipStream_t st) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     QF_HIP(hipStreamIsCapturing(st, &cs));
     if (cs != hipStreamCaptureStatusNone) return 0;
-    if (c->ws_used && c->ws_stream != st) {
-        // the previous stream is capturing into a graph: its decode has not been enqueued
-        // for execution, there is nothing to wait for (and an event recorded into a capture
-        // cannot be waited on from outside it)
-        hipStreamCaptureStatus ps = hipStreamCaptureStatusNone;
-        QF_HIP(hipStreamIsCapturing(c->ws_stream, &ps));
-        if (ps == hipStreamCaptureStatusNone) {
-            QF_HIP(hipEventRecord(c->ws_ev, c->ws_stream));
-            QF_HIP(hipStreamWaitEvent(st, c->ws_ev, 0));
-        }
-    }
+    if (c->ws_used && c->ws_stream != st) QF_HIP(hipStreamWaitEvent(st, c->ws_ev, 0));
     return 0;
 }
 int ws_end(qfec_ctx* c, hipStream_t st) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     QF_HIP(hipStreamIsCapturing(st, &cs));
     if (cs != hipStreamCaptureStatusNone) return 0;
+    // HIP refuses any wait on an event whose stream is capturing at the time of the wait, even
+    // if the event was recorded before the capture began.  So the completion event lives on a
+    // private stream that never captures: it waits for `st` now, while `st` is eager.
+    if (!c->ws_helper) QF_HIP(hipStreamCreateWithFlags(&c->ws_helper, hipStreamNonBlocking));
+    QF_HIP(hipEventRecord(c->ws_tmp, st));
+    QF_HIP(hipStreamWaitEvent(c->ws_helper, c->ws_tmp, 0));
+    QF_HIP(hipEventRecord(c->ws_ev, c->ws_helper));
     c->ws_stream = st;
     c->ws_used = true;
     return 0;
@@ -329,7 +323,7 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
         return 0;
     }
     const int rmax = std::min(k, m);
-    const int rc = stream_decode_rc(k, m, bb, rmax, d_blocks, c->tune);
+    const int rc = stream_decode_rc(rmax);
     const int nchunk = (rmax + rc - 1) / rc;
     const uint8_t* cenc = nullptr;
     int r = get_cenc(c, k, m, &cenc);
@@ -435,7 +429,7 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
                                        (uint8_t*)c->dslots.p, k, bb, G, st, c->tune, true));
         return 0;
     }
-    const int rc = stream_decode_rc(k, m, bb, rmax, d_blocks, c->tune);
+    const int rc = stream_decode_rc(rmax);
     const uint8_t* cenc = nullptr;
     int r = get_cenc(c, k, m, &cenc);
     if (r) return r;
@@ -595,6 +589,25 @@ void note_kernel(const char* name) {
     if (!g_kernels.empty()) g_kernels += " + ";
     g_kernels += n;
 }
+
+void note_grid(const char* name, unsigned grid) {
+    if (!g_grids.empty()) g_grids += " ";
+    g_grids += std::string(name) + "=" + std::to_string(grid);
+}
+
+int resident_blocks(const void* kern, int threads, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, int, size_t>, int> cache;
+    const auto key = std::make_tuple(kern, threads, lds);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, lds) != hipSuccess || n < 1)
+        n = 1;
+    cache.emplace(key, n);
+    return n;
+}
 }  // namespace qfec
 
 // ======================================================================== C ABI
@@ -605,6 +618,8 @@ int qfec_version(void) { return 1; }
 const char* qfec_last_error(void) { return g_err.c_str(); }
 
 const char* qfec_last_kernels(void) { return g_kernels.c_str(); }
+
+const char* qfec_last_grids(void) { return g_grids.c_str(); }
 
 int qfec_set_timing_events(void* start_event, void* stop_event) {
     if (!start_event != !stop_event) return fail(-2, "set both timing events or neither");
@@ -625,14 +640,10 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"dma", &t.dma, 0, 1},                 {"stream", &t.stream, 0, 1},
         {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
         {"const_enc", &t.const_enc, 0, 1},     {"stream_static", &t.stream_static, 0, 1},
-        {"dcol_grid", &t.dcol_grid, 0, 1 << 20}, {"dcol_depth", &t.dcol_depth, 6, 8}, {"dcol_rows", &t.dcol_rows, 8, 16},
-        {"bsyn", &t.bsyn, 0, 1},               {"dcol", &t.dcol, 0, 1},
-        {"dcol_cache", &t.dcol_cache, 0, 3},     {"stream_rc16", &t.stream_rc16, 0, 1},
-        {"ring_nt", &t.ring_nt, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
-        {"psyn", &t.psyn, 0, 1},               {"psyn_depth", &t.psyn_depth, 5, 7}, {"psyn_pf", &t.psyn_pf, 0, 1},
-        {"psyn_jump", &t.psyn_jump, 0, 2},     {"dec_nt", &t.dec_nt, 0, 1},
-        {"psyn_ablate", &t.psyn_ablate, 0, 3},  {"stream_jump", &t.stream_jump, 0, 1},
-        {"wide_st", &t.wide_st, 0, 1},         {"enc_split", &t.enc_split, 0, 1},
+        {"dcol", &t.dcol, 0, 1},               {"dcol_grid", &t.dcol_grid, 0, 1 << 20},
+        {"dcol_depth", &t.dcol_depth, 6, 8},
+        {"bsyn", &t.bsyn, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
+        {"psyn", &t.psyn, 0, 1},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
@@ -642,7 +653,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
     for (const Opt& o : opts) {
         if (strcmp(o.n, name) != 0) continue;
         if (value < o.lo || value > o.hi || (o.p == &t.enc_rc && (value & (value - 1))) ||
-            (o.p == &t.dcol_depth && value == 7) || (o.p == &t.dcol_rows && value != 8 && value != 16) || ((o.p == &t.psyn_depth || o.p == &t.bsyn_depth) && !(value & 1)) || (o.p == &t.psyn_jump && value == 1))
+            (o.p == &t.dcol_depth && value == 7) || (o.p == &t.bsyn_depth && !(value & 1)))
             return fail(-2, std::string("option value out of range: ") + name);
         *o.p = value;
         return 0;
@@ -657,9 +668,9 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
     const std::pair<const char*, int> opts[] = {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
-        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"dcol_grid", t.dcol_grid}, {"dcol_depth", t.dcol_depth}, {"dcol_rows", t.dcol_rows},
-        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"dcol", t.dcol}, {"dcol_cache", t.dcol_cache}, {"stream_rc16", t.stream_rc16},
-        {"ring_nt", t.ring_nt}, {"psyn", t.psyn}, {"psyn_depth", t.psyn_depth}, {"psyn_pf", t.psyn_pf}, {"psyn_jump", t.psyn_jump}, {"dec_nt", t.dec_nt}, {"psyn_ablate", t.psyn_ablate}, {"stream_jump", t.stream_jump}, {"wide_st", t.wide_st}, {"enc_split", t.enc_split},
+        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"dcol", t.dcol},
+        {"dcol_grid", t.dcol_grid}, {"dcol_depth", t.dcol_depth},
+        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"psyn", t.psyn},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb}, {"host_min_groups", t.host_min_groups},
         {"pp_hash", c->pp_hash},
@@ -688,6 +699,7 @@ int qfec_ctx_create(int device, qfec_ctx** out) {
     c->tune.cus = cus > 0 ? cus : 256;
     QF_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     QF_HIP(hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming));
+    QF_HIP(hipEventCreateWithFlags(&c->ws_tmp, hipEventDisableTiming));
     *out = c.release();
     return 0;
 }
@@ -701,10 +713,11 @@ void qfec_ctx_destroy(qfec_ctx* c) {
     for (hipStream_t s : {c->stream, c->s_in, c->s_out})
         if (s) (void)hipStreamSynchronize(s);
     if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
+    if (c->ws_tmp) (void)hipEventDestroy(c->ws_tmp);
     for (int b = 0; b < qfec_ctx::NB; ++b)
         for (hipEvent_t e : {c->ev_in[b], c->ev_done[b], c->ev_out[b]})
             if (e) (void)hipEventDestroy(e);
-    for (hipStream_t s : {c->stream, c->s_in, c->s_out})
+    for (hipStream_t s : {c->stream, c->s_in, c->s_out, c->ws_helper})
         if (s) (void)hipStreamDestroy(s);
     delete c;
 }

@@ -35,33 +35,10 @@ struct Tune {
     int bsyn_depth = 5;       // gf_bsyn: blocks in flight per wave (3..7)
     int psyn = 1;             // QuicR presets with m >= 7 at 1352 B: compiled syndrome decode
                               //   gf_psyn (0: the run-time gf_stream decode)
-    int psyn_depth = 5;       // gf_psyn: blocks in flight per wave (5, 7)
-    int enc_split = 0;        // compiled preset encodes with m > 10 in two output chunks
-    int wide_st = 0;          // gf_psyn: recovered blocks assembled in LDS and written with
-                              //   8-byte stores of contiguous bytes (3 per block, not 16)
-    int stream_jump = 1;      // gf_stream decode (bb = 1352, <= 8 outputs per unit): run-time
-                              //   products by nibble jumps (gf_winjump.h) instead of trees
-    int psyn_ablate = 0;      // timing probe only (wrong results): gf_psyn without its stores
-                              //   (1), without its arithmetic (2), without both (3)
-    int dec_nt = 1;           // gf_bsyn / gf_psyn: recovered blocks stored non-temporal
-    int psyn_jump = 2;        // gf_psyn: solve products by two nibble jumps into leaf tables
-                              //   (gf_winjump.h; 0: a 256-way tree of uniform branches; 1,
-                              //   one 256-leaf jump + scatter, measured slower and removed)
-    int psyn_pf = 0;          // gf_psyn: block b + 1 read into registers while block b is
-                              //   combined (0: read when consumed, fewer VGPRs)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16
                               //   rows; 0: gf_apply)
     int dcol_grid = 0;        // gf_dcol: grid cap in workgroups (0: CUs x per-CU fit)
-    int dcol_depth = 6;       // gf_dcol: blocks in flight per wave (6, or 8 with the default
-                              //   cache policy)
-    int dcol_rows = 16;       // gf_dcol encode: parity rows per wave (16, or 8: two waves per
-                              //   tile at four waves per SIMD)
-    int dcol_cache = 2;       // gf_dcol cache policy: encode 0 / 1 cached loads and non-temporal
-                              //   stores, 2 / 3 cached loads and stores; decode (stores
-                              //   plain) non-temporal loads for 0 / 2, cached 1 / 3
-    int stream_rc16 = 0;      // gf_stream decode of 9..16 losses as one 16-block unit (0: two
-                              //   units of 8, the second empty for <= 8 losses and skipped)
-    int ring_nt = 1;          // gf_ring (B/C encode) parity stores non-temporal (0: plain)
+    int dcol_depth = 6;       // gf_dcol: blocks in flight per wave (6 or 8; two waves per SIMD)
     int host_chunk_mb = 64;   // host-pointer batches: chunk size
     int host_min_groups = 512;  // host-pointer batches: at least this many groups per chunk
                                 //   (capped at 2 GiB of staging per buffer)
@@ -69,6 +46,13 @@ struct Tune {
 
 // Records the name of a kernel a call launched (qfec_last_kernels(), per thread).
 void note_kernel(const char* name);
+// Records the grid (workgroups) a persistent kernel was launched with (qfec_last_grids(),
+// per thread, "name=grid" entries).
+void note_grid(const char* name, unsigned grid);
+
+// Workgroups of `kern` one CU holds at once (the runtime's occupancy answer), cached per
+// (kernel, threads, LDS bytes); thread-safe.
+int resident_blocks(const void* kern, int threads, size_t lds);
 
 // Kernel timing hook (qfec_set_timing_events, per thread).  While a stop event is set, each
 // engine call records `start` at the start of its first kernel and `stop` at the end of

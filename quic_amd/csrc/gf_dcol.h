@@ -126,30 +126,22 @@ struct DcShape {
 // CACHE: bit 0 = the DMA loads are plain (cached) instead of non-temporal, bit 1 = the
 // stores are plain instead of non-temporal.  Neighbouring tiles' 256-byte envelopes share
 // cache lines, which a non-temporal load evicts first.
-// RW: parity rows per wave.  16: one wave per (group, tile) computes all rows (about 190
-// VGPRs, two waves per SIMD).  8 (encode): a unit is (group, tile, half); the two halves of
-// a tile are neighbouring waves of one workgroup streaming the same bytes (the second read
-// hits L2), each builds the block's window and applies 8 rows, in <= 128 VGPRs: four waves
-// per SIMD.
-template <int S, int D, bool DECODE, int CACHE, int RW = 16>
-__global__ __launch_bounds__(kDcWaves * 64, RW == 16 ? 2 : 3) void gf_dcol_kernel(
+// About 190 VGPRs: two waves per SIMD.  Block b + 1 is read from LDS into registers while
+// block b is combined (prefetch).
+template <int S, int D, bool DECODE, int CACHE>
+__global__ __launch_bounds__(kDcWaves * 64, 2) void gf_dcol_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout,
     const uint8_t* __restrict__ cenc, long long groups, int rmax, long long in_bytes,
     long long tab_gstride, long long out_gstride) {
     using SH = DcShape<S>;
     constexpr int KC = 128, MC = 16;
-    constexpr int NH = MC / RW;                      // units per tile
-    static_assert((RW == 16 || RW == 8) && (!DECODE || RW == 16), "rows per wave");
+    constexpr int RW = MC;                           // parity rows per wave: all of them
     constexpr int BB = SH::BB, NW = SH::NW, NWF = SH::NWF, NT = SH::NT;
     constexpr int SEGL = SH::SEGL, SEGB = SH::SEGB, TAILL = SH::TAILL, BUFB = SH::BUFB;
     constexpr int NDMA = SH::NDMA;
     constexpr int NBUF = D + 1;                      // D in flight + the one being read
-    // RW = 16 reads block b + 1 into registers while block b is combined (prefetch); RW = 8
-    // reads each block when its turn comes (16 fewer VGPRs), so when block b is awaited the
-    // D blocks issued after it are younger
-    constexpr bool PF = RW == 16;
-    constexpr int WAITN = PF ? (D - 1) * NDMA : D * NDMA;   // younger than the awaited block
+    constexpr int WAITN = (D - 1) * NDMA;            // younger than the awaited block b + 1
     constexpr int NSTMIN = 64 - WAITN;               // stores a unit ends with, at least
     static_assert(WAITN + NSTMIN >= 63 && WAITN <= 63 && D >= 2 && KC % 4 == 0 && D <= KC / 2,
                   "pipeline");
@@ -165,7 +157,7 @@ __global__ __launch_bounds__(kDcWaves * 64, RW == 16 ? 2 : 3) void gf_dcol_kerne
     const unsigned lwg = xcd * q8 + min(xcd, r8) + (hb >> 3);
     const long long W = (long long)nwg * kDcWaves;
     const long long u0 = (long long)lwg * kDcWaves + wv;
-    const long long NU = groups * NT * NH;
+    const long long NU = groups * NT;
     if (u0 >= NU) return;
     const int cnt = __builtin_amdgcn_readfirstlane((int)((NU - 1 - u0) / W + 1));
 
@@ -192,7 +184,7 @@ __global__ __launch_bounds__(kDcWaves * 64, RW == 16 ? 2 : 3) void gf_dcol_kerne
     };
     auto make_unit = [&](int i, Unit& un, uint32_t& v0, uint32_t& v1) __attribute__((always_inline)) {
         un.none = i >= cnt;
-        const long long u = (un.none ? u0 : u0 + (long long)i * W) / NH;   // (group, tile)
+        const long long u = un.none ? u0 : u0 + (long long)i * W;   // (group, tile)
         const long long g = u / NT;
         const int p = (int)(u - g * NT);
         un.src = in + g * (long long)KC * BB;
@@ -297,15 +289,6 @@ __global__ __launch_bounds__(kDcWaves * 64, RW == 16 ? 2 : 3) void gf_dcol_kerne
         if (rd_off == NBUF * BUFB) rd_off = 0;
         read_block(nlo, nhi);
     };
-    // (no prefetch) wait for block b itself and read it into (lo, hi)
-    auto this_block = [&](auto early, uint32_t (&lo)[8], uint32_t (&hi)[8])
-                          __attribute__((always_inline)) {
-        if constexpr (decltype(early)::value) dc_wait_vmcnt<63>();
-        else dc_wait_vmcnt<WAITN>();
-        read_block(lo, hi);
-        rd_off += BUFB;
-        if (rd_off == NBUF * BUFB) rd_off = 0;
-    };
 
     // ---- prologue: unit 0's first D rows, then the stores a previous unit would have issued
     // (empty range), so every unit's blocks 1 .. D - 1 have at least NSTMIN stores younger
@@ -321,16 +304,12 @@ __global__ __launch_bounds__(kDcWaves * 64, RW == 16 ? 2 : 3) void gf_dcol_kerne
     }
     asm volatile("" ::: "memory");
     uint32_t lo0[8], hi0[8], lo1[8], hi1[8];
-    if constexpr (PF) {
-        dc_wait_vmcnt<WAITN>();
-        read_block(lo0, hi0);
-    }
+    dc_wait_vmcnt<WAITN>();
+    read_block(lo0, hi0);
 
 #pragma unroll 1
     for (int i = 0; i < cnt; ++i) {
-        const long long uh = u0 + (long long)i * W;
-        const int h = (int)(uh % NH);                  // rows h * RW .. of the tile
-        const long long u = uh / NH;
+        const long long u = u0 + (long long)i * W;
         const long long g = u / NT;
         const int p = (int)(u - g * NT);
         const uint8_t* tb = tab + (DECODE ? g * tab_gstride : 0);
@@ -344,10 +323,9 @@ __global__ __launch_bounds__(kDcWaves * 64, RW == 16 ? 2 : 3) void gf_dcol_kerne
 
         // data row x (compile time): issue stream position x + D, read block x + 1, and
         // every row's windowed apply of block x
-        auto step = [&](auto hc, auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
+        auto step = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
                         uint32_t (&nhi)[8]) __attribute__((always_inline)) {
             constexpr int x = decltype(xc)::value;
-            constexpr int H0 = decltype(hc)::value * RW;   // the unit's first row
             if constexpr (x + D < KC) {
                 issue_row(std::integral_constant<int, x + D>{}, cu, vc0, vc1, rw_c, rn_c);
             } else if constexpr (!DECODE) {
@@ -356,41 +334,27 @@ __global__ __launch_bounds__(kDcWaves * 64, RW == 16 ? 2 : 3) void gf_dcol_kerne
                 issue_tail(x + D);
             }
             uint32_t w8[8];
-            if constexpr (PF) {
-                next_block(std::bool_constant<(x + 1 <= D - 1)>{}, nlo, nhi);
-                realign(lo, hi, w8);
-            } else {
-                // block x was issued before the previous unit's stores when x < D
-                uint32_t clo[8], chi[8];
-                this_block(std::bool_constant<(x <= D - 1)>{}, clo, chi);
-                realign(clo, chi, w8);
-            }
+            next_block(std::bool_constant<(x + 1 <= D - 1)>{}, nlo, nhi);
+            realign(lo, hi, w8);
             Win win;
             win_build(w8, win);
             static_for<RW>([&](auto yc) __attribute__((always_inline)) {
                 constexpr int y = decltype(yc)::value;
-                win_apply<cauchy_coef(MC, H0 + y, x)>(acc[y], win);
+                win_apply<cauchy_coef(MC, y, x)>(acc[y], win);
             });
         };
-        // the unit's rows are compile-time in each copy of the block loop (one copy per half)
-        auto block_loop = [&](auto hc) __attribute__((always_inline)) {
-            static_for<KC>([&](auto xc) __attribute__((always_inline)) {
-                // accumulators opaque at every block boundary: with constant coefficients the
-                // XOR reassociation would otherwise merge the blocks' sums and keep every
-                // block's window live; and nothing is scheduled across blocks (register
-                // pressure)
+        static_for<KC>([&](auto xc) __attribute__((always_inline)) {
+            // accumulators opaque at every block boundary: with constant coefficients the XOR
+            // reassociation would otherwise merge the blocks' sums and keep every block's
+            // window live; and nothing is scheduled across blocks (register pressure)
 #pragma unroll
-                for (int y = 0; y < RW; ++y)
+            for (int y = 0; y < RW; ++y)
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[y][r]));
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (decltype(xc)::value % 2 == 0) step(hc, xc, lo0, hi0, lo1, hi1);
-                else step(hc, xc, lo1, hi1, lo0, hi0);
-            });
-        };
-        if constexpr (NH == 1) block_loop(std::integral_constant<int, 0>{});
-        else if (h == 0) block_loop(std::integral_constant<int, 0>{});
-        else block_loop(std::integral_constant<int, 1>{});
+                for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[y][r]));
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (decltype(xc)::value % 2 == 0) step(xc, lo0, hi0, lo1, hi1);
+            else step(xc, lo1, hi1, lo0, hi0);
+        });
 
         asm volatile("" ::: "memory");   // stores stay in issue order among the DMAs
         const int lane_e = dc_lane_here();
@@ -422,7 +386,7 @@ __global__ __launch_bounds__(kDcWaves * 64, RW == 16 ? 2 : 3) void gf_dcol_kerne
             static_assert(RW * 8 >= NSTMIN, "store count");
 #pragma unroll
             for (int y = 0; y < RW; ++y)
-                store_out(out + g * out_gstride + (long long)(h * RW + y) * BB, true, acc[y]);
+                store_out(out + g * out_gstride + (long long)y * BB, true, acc[y]);
         } else {
             const int ne = cu.len - KC;
             const int n = min((int)dc_cload_u32((const uint8_t*)nout, 4 * g), rmax);
@@ -431,8 +395,8 @@ __global__ __launch_bounds__(kDcWaves * 64, RW == 16 ? 2 : 3) void gf_dcol_kerne
             auto extra = [&](int e, uint32_t (&lo)[8], uint32_t (&hi)[8], uint32_t (&nlo)[8],
                              uint32_t (&nhi)[8]) __attribute__((always_inline)) {
                 issue_tail(KC + e + D);
-                next_block(std::false_type{}, nlo, nhi);
                 WZ v;
+                next_block(std::false_type{}, nlo, nhi);
                 realign(lo, hi, v.W8);
                 const int row = dc_cload_u8(tb, syn::kERow + e);
                 if (row >= KC) {
@@ -544,13 +508,10 @@ constexpr int kDcolS = 1126;   // bb = 9008: 9000-byte payloads (BASELINE config
     dim3 grid, size_t lds, hipStream_t st, const uint8_t *in, uint8_t *out, const uint8_t *tab, \
         const uint8_t *slots, const int32_t *nout, const uint8_t *cenc, long long groups,       \
         int rmax, long long in_bytes, long long tab_gstride, long long out_gstride
-hipError_t dcol_go_e61(QD_LAUNCH_ARGS);
 hipError_t dcol_go_e63(QD_LAUNCH_ARGS);
 hipError_t dcol_go_e83(QD_LAUNCH_ARGS);
 hipError_t dcol_go_d62(QD_LAUNCH_ARGS);
-hipError_t dcol_go_d63(QD_LAUNCH_ARGS);
 hipError_t dcol_go_d82(QD_LAUNCH_ARGS);
-hipError_t dcol_go_h43(QD_LAUNCH_ARGS);
 
 #define QD_DEFINE_GO(NAME, DV, DEC, C, ...)                                                     \
     hipError_t NAME(QD_LAUNCH_ARGS) {                                                           \

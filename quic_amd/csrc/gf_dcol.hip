@@ -9,9 +9,8 @@ bool gf_dcol_supported(int k, int m, int bb, const Tune& t) {
     return t.dcol && t.const_enc && k == 128 && m == 16 && bb == 8 * kDcolS;
 }
 
-// groups: units per tile included (x2 for 8 rows per wave); wg_cu: workgroups of 4 waves a CU
-// holds by registers (2 at <= 256 VGPRs, 4 at <= 128), LDS permitting
-static unsigned dcol_grid(long long groups, const Tune& t, size_t lds, int wg_cu = 2) {
+// wg_cu: workgroups of 4 waves a CU holds by registers (2 at <= 256 VGPRs), LDS permitting
+static unsigned dcol_grid(long long groups, const Tune& t, size_t lds, int wg_cu) {
     using SH = DcShape<kDcolS>;
     const long long units = groups * SH::NT;
     const long long want = (units + kDcWaves - 1) / kDcWaves;
@@ -28,24 +27,21 @@ hipError_t launch_gf_dcol_encode(const uint8_t* in, uint8_t* out, int k, int m, 
     if (!gf_dcol_supported(k, m, bb, t)) return hipErrorInvalidValue;
     if (((uintptr_t)in & 15) != 0) return hipErrorInvalidValue;
     using SH = DcShape<kDcolS>;
-    const int rows = t.dcol_rows;                    // 8: two units per tile, depth 4
-    const int D = rows == 8 ? 4 : t.dcol_depth;
-    if (D != 4 && D != 6 && D != 8) return hipErrorInvalidValue;
+    const int D = t.dcol_depth;
+    if (D != 6 && D != 8) return hipErrorInvalidValue;
     const size_t lds = (size_t)kDcWaves * (D + 1) * SH::BUFB;
-    const unsigned grid = dcol_grid(groups * (16 / rows), t, lds, rows == 8 ? 4 : 2);
+    const unsigned grid = dcol_grid(groups, t, lds, 2);
     const long long waves = (long long)grid * kDcWaves;
-    if ((groups * SH::NT * (16 / rows) + waves - 1) / waves >= (1LL << 31))
-        return hipErrorInvalidValue;
-    note_kernel(rows == 8 ? "gf_dcol_kernel<encode,k128m16,rows8>" : "gf_dcol_kernel<encode,k128m16>");
+    if ((groups * SH::NT + waves - 1) / waves >= (1LL << 31)) return hipErrorInvalidValue;
+    note_kernel("gf_dcol_kernel<encode,k128m16>");
+    note_grid("gf_dcol_kernel<encode>", grid);
     const long long in_bytes = groups * (long long)k * bb;
 #define QD_ENC(NAME) return NAME(dim3(grid), lds, st, in, out, nullptr, nullptr, nullptr, nullptr, \
                              groups, 0, in_bytes, 0LL, out_gstride)
-    // dcol_cache <= 1: cached loads, non-temporal stores; >= 2: cached loads and stores
-    // (default: the parity's partial cache lines at tile edges merge in L2 instead of going
-    // to HBM twice; D encode 20.3 -> 16.5 ms, non-temporal loads too: 21.7 ms)
-    if (t.dcol_rows == 8) QD_ENC(dcol_go_h43);
+    // cached loads and stores: the parity's partial cache lines at tile edges merge in L2
+    // instead of going to HBM twice (D encode 20.3 -> 16.5 ms; non-temporal loads too: 21.7
+    // ms)
     if (D == 8) QD_ENC(dcol_go_e83);
-    if (t.dcol_cache <= 1) QD_ENC(dcol_go_e61);   // 0 measured 21.7 ms: not kept
     QD_ENC(dcol_go_e63);
 #undef QD_ENC
     return hipGetLastError();
@@ -66,16 +62,17 @@ hipError_t launch_gf_dcol_syndrome(const uint8_t* in, uint8_t* out, const uint8_
     const int D = t.dcol_depth;
     if (D != 6 && D != 8) return hipErrorInvalidValue;
     const size_t lds = (size_t)kDcWaves * (D + 1) * SH::BUFB;
-    const unsigned grid = dcol_grid(groups, t, lds);
+    const unsigned grid = dcol_grid(groups, t, lds, 2);
     const long long waves = (long long)grid * kDcWaves;
     if ((groups * SH::NT + waves - 1) / waves >= (1LL << 31)) return hipErrorInvalidValue;
     note_kernel("gf_dcol_kernel<decode,k128m16>");
-    // decode stores are plain; loads non-temporal (dcol_cache 0, 2) or cached (1, 3)
+    note_grid("gf_dcol_kernel<decode>", grid);
+    // decode: non-temporal loads, plain stores (cached loads: 1.011x instead of 1.167x the
+    // algorithmic reads, but 18.3 vs 16.9 ms and the next encode over-reads)
     const long long in_bytes = groups * (long long)k * bb;
 #define QD_DEC(NAME) return NAME(dim3(grid), lds, st, in, out, tab, slots, nout, cenc, groups, \
                              rmax, in_bytes, tab_gstride, out_gstride)
     if (D == 8) QD_DEC(dcol_go_d82);
-    if (t.dcol_cache & 1) QD_DEC(dcol_go_d63);
     QD_DEC(dcol_go_d62);
 #undef QD_DEC
     return hipGetLastError();

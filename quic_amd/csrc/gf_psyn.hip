@@ -303,13 +303,10 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
     if ((((uintptr_t)in) & 15) || ((((uintptr_t)tab) | (uintptr_t)cenc | (uintptr_t)slots) & 3))
         return hipErrorInvalidValue;
     using SH = PsynShape<kPsynS>;
-    const int D = t.psyn_depth;
-    if ((D != 5 && D != 7) || (t.psyn_jump != 0 && t.psyn_jump != 2)) return hipErrorInvalidValue;
     PsynLaunch a;
     a.in = in, a.out = out, a.tab = tab, a.cenc = cenc, a.slots = slots, a.nout = nout;
     a.groups = groups, a.rmax = rmax, a.out_gstride = out_gstride, a.st = st, a.t = &t, a.k = k;
-    a.wide = t.psyn_jump == 2 && t.wide_st != 0 && (((uintptr_t)out | (uintptr_t)out_gstride) & 7) == 0;
-    a.lds = (size_t)kPsynWaves * ((D + 1) * SH::BUFB + (a.wide ? kPsynStage : 0));
+    a.lds = (size_t)kPsynWaves * (5 + 1) * SH::BUFB;   // ring depth 5
     note_kernel("gf_psyn_kernel<decode,preset>");
     switch (k * 256 + m) {
         case 10 * 256 + 10: return psyn_go_1010(a);

@@ -102,13 +102,10 @@ constexpr int kMirror = 2;                 // mirrored slots: a block (<= 2 KiB 
 // accumulator (gf_winjump.h wz_mul_acc_rt) instead of two 16-way uniform branch trees.
 // WIDE (compiled encode, S = 169): each output block is assembled in a per-wave LDS staging
 // buffer (inline-asm ds ops) and written with 3 dwordx2 stores of contiguous bytes instead
-// of 8 x (b32 + b8) sub-row stores (gf_psyn.h, wide_st option).
+// of 8 x (b32 + b8) sub-row stores (the (5, 5) encode).
 constexpr int kStreamStage = 1360;
-// MF (compiled encode): the code's m when the outputs are cut into two chunks of RC rows
-// (units (group, chunk) on neighbouring waves, the second re-reading the group through L2):
-// half the accumulators, so more waves per SIMD for m > 10.  0: one chunk, m = RC.
 template <int RC, int S, bool DECODE, int RCPT = (RC < 4 ? 4 : RC), int KC = 0, bool NJ = false,
-          bool WIDE = false, int MF = 0>
+          bool WIDE = false>
 __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
@@ -127,7 +124,15 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     constexpr int SPR = S ? 1 + ((S >> 1) & 1) + (S & 1) : 3;
     constexpr int SAUX = DECODE ? 0 : 2;   // encode's dense parity stream: nt stores
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = threadIdx.x & 63;
+    // the lane id, recomputed where it is used (v_mbcnt): nothing lane-derived stays live
+    // across the block loop (register pressure of the compiled encodes with many outputs)
+    auto lane_here = []() __attribute__((always_inline)) -> int {
+        int l = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+#endif
+        return l;
+    };
     const int w = wave_id();
     const int RB = R * 1024;
     uint8_t* ring = smem + (size_t)w * (R + kMirror) * 1024;
@@ -145,7 +150,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const int gb = k * BB;
     const int skew8 = (gb & 15) ? 8 : 0;               // groups may start 8 mod 16
     const int NP = (gb + skew8 + 1023) >> 10;          // pieces per unit
-    const int c = lane < NW ? lane : NW - 1;           // idle lanes shadow the last word
+    // column word of a lane (idle lanes shadow the last word)
+    auto col_here = [&]() __attribute__((always_inline)) -> int { return min(lane_here(), NW - 1); };
 
     // ---- issue side (wave-uniform): next piece iss_p of the stream, into slot iss_slot
     int iss_p = 0, iss_slot = 0;
@@ -179,6 +185,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     const uint8_t* isrc = unit_src(iss_u < u_end ? iss_u : g0, ilast, inrec);
 
     auto issue_one = [&]() {
+        const int lane = lane_here();
         const int off = min(iss_p * 1024 + lane * 16, ilast);   // last piece: clamp inside
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void*)isrc, 0, inrec, 0x00020000);
@@ -229,7 +236,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
     auto read_block = [&](uint32_t bp, uint32_t (&lo)[8], uint32_t (&hi)[8]) {
         // the lane's byte offset, opaque to the optimiser: in the fully unrolled (KC > 0)
         // form it would otherwise precompute every block's addresses up front
-        uint32_t c4 = 4u * (uint32_t)c;
+        uint32_t c4 = 4u * (uint32_t)col_here();
         if constexpr (KC > 0) asm volatile("" : "+v"(c4));
         const uint8_t* L = ring + bp + c4;
 #pragma unroll
@@ -283,7 +290,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     cB[q] = cw[(k > 1 ? 1 : 0) * NCW + q];
                 }
             }
-            auto step = [&](auto xc, auto chc, uint32_t (&lo)[8], uint32_t (&hi)[8],
+            auto step = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8],
                             uint32_t (&nlo)[8], uint32_t (&nhi)[8], uint32_t (&cc)[NCW]) {
                 const int x = xc;
                 const uint32_t bn = next_pos(bpos);
@@ -305,11 +312,9 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     // is P0, all coefficients 1 (cauchy_256.cpp:1519-1523)
                     Win win;
                     win_build(v.W8, win);
-                    constexpr int MFC = MF ? MF : RC, J0 = decltype(chc)::value * RC;
                     static_for<RC>([&](auto jc) __attribute__((always_inline)) {
                         constexpr int j = decltype(jc)::value;
-                        if constexpr (J0 + j < MFC)
-                            win_apply<cauchy_coef(MFC, J0 + j, decltype(xc)::value)>(acc[j], win);
+                        win_apply<cauchy_coef(RC, j, decltype(xc)::value)>(acc[j], win);
                     });
                     return;
                 }
@@ -339,53 +344,34 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
                     }
                 }
             };
-            using I0 = std::integral_constant<int, 0>;
             if constexpr (KC > 0) {
-                auto blocks = [&](auto chc) {
-                    static_for<KC>([&](auto xc) {
-                        // the accumulators are opaque at every block boundary: with all
-                        // coefficients constant, the XOR reassociation would otherwise
-                        // flatten the blocks' sums into one tree and keep every block's W/Z
-                        // live (~490 VGPRs)
+                // the block loop inline, not through a lambda (the fully unrolled 250-block
+                // loop of (250, 5) spills to scratch through one)
+                static_for<KC>([&](auto xc) {
+                    // the accumulators are opaque at every block boundary: with all
+                    // coefficients constant, the XOR reassociation would otherwise flatten the
+                    // blocks' sums into one tree and keep every block's W/Z live (~490 VGPRs)
 #pragma unroll
-                        for (int j = 0; j < RC; ++j)
+                    for (int j = 0; j < RC; ++j)
 #pragma unroll
-                            for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
-                        if constexpr (decltype(xc)::value % 2 == 0)
-                            step(xc, chc, lo0, hi0, lo1, hi1, cA);
-                        else
-                            step(xc, chc, lo1, hi1, lo0, hi0, cB);
-                    });
-                };
-                if constexpr (MF > RC) {
-                    static_assert(MF <= 2 * RC, "two chunks");
-                    if (ch == 0) blocks(I0{});
-                    else blocks(std::integral_constant<int, 1>{});
-                } else {
-                    // one chunk: the block loop inline, not through the lambda (the fully
-                    // unrolled 250-block loop of (250, 5) spills to scratch through it)
-                    static_for<KC>([&](auto xc) {
-#pragma unroll
-                        for (int j = 0; j < RC; ++j)
-#pragma unroll
-                            for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
-                        if constexpr (decltype(xc)::value % 2 == 0)
-                            step(xc, I0{}, lo0, hi0, lo1, hi1, cA);
-                        else
-                            step(xc, I0{}, lo1, hi1, lo0, hi0, cB);
-                    });
-                }
+                        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(acc[j][r]));
+                    if constexpr (decltype(xc)::value % 2 == 0)
+                        step(xc, lo0, hi0, lo1, hi1, cA);
+                    else
+                        step(xc, lo1, hi1, lo0, hi0, cB);
+                });
             } else {
 #pragma unroll 1
                 for (int x = 0; x < k; x += 2) {
-                    step(x, I0{}, lo0, hi0, lo1, hi1, cA);
-                    if (x + 1 < k) step(x + 1, I0{}, lo1, hi1, lo0, hi0, cB);
+                    step(x, lo0, hi0, lo1, hi1, cA);
+                    if (x + 1 < k) step(x + 1, lo1, hi1, lo0, hi0, cB);
                 }
             }
             asm volatile("" ::: "memory");   // stores stay in issue order among the DMAs
             // ---- outputs: fixed instruction count per output (dropped lanes, no branches).
             // Lane offsets 4c (full words) and the tail lane's, sub-row in the scalar offset:
             // two address VGPRs, opaque so they are not hoisted as 8 x RC precomputed ones.
+            const int lane = lane_here(), c = min(lane, NW - 1);
             uint32_t vo = lane < NWF ? 4u * (uint32_t)c : kSDrop;
             uint32_t vt = lane == NWF && NWF < NW ? 4u * (uint32_t)c : kSDrop;
             asm volatile("" : "+v"(vo), "+v"(vt));
@@ -785,8 +771,6 @@ bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& 
     return true;
 }
 
-static bool wide_enc_want(const Tune& t) { return t.wide_st != 0; }
-
 hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef,
                             const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
                             long long groups, int rc, int rmax, long long coef_gstride,
@@ -797,11 +781,10 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     if (((uintptr_t)in & 15) != 0 || ((uintptr_t)slots & 3) != 0) return hipErrorInvalidValue;
     const int R = t.stream_ring;
     if (R < 4 || R > 36) return hipErrorInvalidValue;
-    // (not (250, 5): its fully unrolled 250-block loop with the staging spills to scratch)
-    const bool wide_enc = !decode && t.wide_st && t.const_enc && gf_stream_compiled(k, m, bb) &&
-                          k <= 32 &&
-                          bb == 1352 && (((uintptr_t)out | (uintptr_t)out_gstride) & 7) == 0 &&
-                          !(t.stream_static && k == 32 && m == 4);
+    // wide (LDS-staged 8-byte) parity stores: measured faster only for the (5, 5) encode
+    // (0.203 -> 0.180 ms; within +-5 % on the other presets)
+    const bool wide_enc = !decode && t.const_enc && k == 5 && m == 5 && bb == 1352 &&
+                          (((uintptr_t)out | (uintptr_t)out_gstride) & 7) == 0;
     const size_t lds = (size_t)kStreamWaves * ((R + kMirror) * 1024 + (wide_enc ? kStreamStage : 0));
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int per_cu = (int)((160 * 1024) / lds);
@@ -809,11 +792,7 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     // of exactly m outputs), decode chunks of rc for rmax > rc
     const int s = bb / 8;
     const bool compiled = !decode && t.const_enc && gf_stream_compiled(k, m, bb);
-    // compiled encodes of m > 10 in two chunks (enc_split option): (10,15) (15,15) as 8 + 7
-    // rows, (10,20) as 10 + 10
-    const bool split = compiled && t.enc_split && m > 10 && bb == 1352 && !wide_enc_want(t);
     const int nchunk = decode ? (rmax + rc - 1) / rc
-                       : split ? 2
                               : (compiled || m <= 8 || (rc == 16 && m <= 16)) ? 1 : (m + 7) / 8;
     const long long units = groups * nchunk;
     const long long want = (units + kStreamWaves - 1) / kStreamWaves;
@@ -847,7 +826,6 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         case 2: QS_GO(2, SV, true, 4, 0); break;          \
         case 4: QS_GO(4, SV, true, 4, 0); break;          \
         case 8: QS_GO(8, SV, true, 8, 0); break;          \
-        case 16: QS_GO(16, SV, true, 16, 0); break;       \
         default: return hipErrorInvalidValue;             \
     }
     // encode: one output per register set, RC = m; the table row stride is max(4, rc)
@@ -880,19 +858,14 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
                        dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax, \
                        coef_gstride, out_gstride)
         note_kernel("gf_ring_kernel<encode,k32m4>");
-        if (t.ring_nt) QR_GO(4, false, 4, true);
-        else QR_GO(4, false, 4, false);
+        QR_GO(4, false, 4, true);   // nt parity stores (plain: 0.673 vs 0.578 ms)
 #undef QR_GO
         return hipGetLastError();
     }
     if (decode) {
         if (s == 169) {
             note_kernel("gf_stream_kernel<decode>");
-            if (t.stream_jump && rc <= 8) {
-                QS_DECJ(169)
-            } else {
-                QS_DEC(169)
-            }
+            QS_DECJ(169)
         } else {
             note_kernel("gf_stream_kernel<decode,s>");
             QS_DEC(0)
@@ -902,35 +875,10 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
             // BASELINE configs B/C and the QuicR presets at 1350-byte payloads: the code is
             // fixed at compile time (windowed form, every output in one unit)
             note_kernel("gf_stream_kernel<encode,compiled>");
-            if (split) {
-#define QS_GOS(RCV, RCPV, KCV, MFV)                                                            \
-    qlaunch((gf_stream_kernel<RCV, 169, false, RCPV, KCV, false, false, MFV>), dim3(grid),     \
-            dim3(threads), lds, st, in, out, coef, slots, nout, groups, k, m, rmax,            \
-            coef_gstride, out_gstride, R, s, nchunk)
-                switch (k * 256 + m) {
-                    case 10 * 256 + 15: QS_GOS(8, 8, 10, 15); break;
-                    case 10 * 256 + 20: QS_GOS(10, 12, 10, 20); break;
-                    case 15 * 256 + 15: QS_GOS(8, 8, 15, 15); break;
-                    default: return hipErrorInvalidValue;
-                }
-#undef QS_GOS
-                return hipGetLastError();
-            }
             if (wide_enc) {
-#define QS_GOW(RCV, RCPV, KCV)                                                                 \
-    qlaunch((gf_stream_kernel<RCV, 169, false, RCPV, KCV, false, true>), dim3(grid),           \
-            dim3(threads), lds, st, in, out, coef, slots, nout, groups, k, m, rmax,            \
-            coef_gstride, out_gstride, R, s, nchunk)
-                switch (k * 256 + m) {
-                    case 32 * 256 + 4: QS_GOW(4, 4, 32); break;
-                    case 5 * 256 + 5: QS_GOW(5, 8, 5); break;
-                    case 10 * 256 + 10: QS_GOW(10, 12, 10); break;
-                    case 10 * 256 + 15: QS_GOW(15, 16, 10); break;
-                    case 10 * 256 + 20: QS_GOW(20, 20, 10); break;
-                    case 15 * 256 + 15: QS_GOW(15, 16, 15); break;
-                    default: return hipErrorInvalidValue;
-                }
-#undef QS_GOW
+                qlaunch((gf_stream_kernel<5, 169, false, 8, 5, false, true>), dim3(grid),
+                        dim3(threads), lds, st, in, out, coef, slots, nout, groups, k, m, rmax,
+                        coef_gstride, out_gstride, R, s, nchunk);
                 return hipGetLastError();
             }
             switch (k * 256 + m) {

@@ -287,6 +287,17 @@ def last_kernels():
     return v.decode() if v else ""
 
 
+def last_grids():
+    """{kernel: workgroups} of the persistent kernels the calling thread's last engine call
+    launched (qfec_last_grids)."""
+    v = load().qfec_last_grids()
+    out = {}
+    for item in (v.decode() if v else "").split():
+        name, _, grid = item.partition("=")
+        out[name] = int(grid)
+    return out
+
+
 def _hptr(t):
     import torch
     if not isinstance(t, torch.Tensor) or t.is_cuda or not t.is_contiguous():

@@ -459,10 +459,22 @@ OPTION_SETS = [
     {"dma": 0}, {"stream": 0}, {"stream": 0, "pd": 1}, {"stream": 0, "pd": 3},
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
     {"stream_ring": 36}, {"host_chunk_mb": 1, "host_min_groups": 1}, {"const_enc": 0},
-    {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 3}, {"dcol": 0}, {"dcol_cache": 0},
-    {"dcol_cache": 1}, {"dcol_cache": 3}, {"stream_rc16": 1}, {"ring_nt": 0}, {"dec_nt": 0},
-    {"stream_jump": 0}, {"bsyn": 0, "stream_jump": 1}, {"wide_st": 1}, {"enc_split": 1},
+    {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 3}, {"dcol": 0}, {"dcol_depth": 8},
+    {"psyn": 0},
 ]
+
+
+# measured-and-rejected variants and timing probes are not options of the product ABI
+# (DESIGN.md section 3.7): qfec_ctx_set_option refuses them with -2
+REMOVED_OPTIONS = ["psyn_ablate", "enc_split", "wide_st", "stream_rc16", "dcol_rows", "dcol_cache",
+                   "psyn_jump", "psyn_pf", "psyn_depth", "ring_nt", "dec_nt", "stream_jump"]
+
+
+@pytest.mark.parametrize("name", REMOVED_OPTIONS)
+def test_removed_options_refused(engine, name):
+    with pytest.raises(fec.FecError) as e:
+        engine.set_option(name, 1)
+    assert e.value.rc == -2
 
 
 @pytest.mark.parametrize("opts", OPTION_SETS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
@@ -733,20 +745,17 @@ PRESETS = [(5, 5), (10, 10), (10, 15), (10, 20), (15, 15), (250, 5)]   # quic_fe
 PSYN = {(10, 10), (10, 15), (10, 20), (15, 15)}   # m >= 7: gf_psyn's compiled syndrome decode
 
 
-@pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0, "stream_rc16": 1},
-                                  {"psyn": 0, "stream_jump": 0}, {"wide_st": 1},
-                                  {"wide_st": 1, "stream_grid": 1, "dec_nt": 1},
-                                  {"enc_split": 1}, {"enc_split": 1, "stream_grid": 1}],
-                         ids=["default", "grid1", "runtime_rc16", "runtime_trees", "wide",
-                              "wide_grid1_nt", "split", "split_grid1"])
+@pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0},
+                                  {"psyn": 0, "stream_grid": 1}],
+                         ids=["default", "grid1", "runtime", "runtime_grid1"])
 @pytest.mark.parametrize("k,m", PRESETS)
 def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
     """QuicR's negotiated configurations with 1350-byte payloads (bb = 1352): odd k puts every
     other group 8 bytes off a 16-byte boundary, m > 8 and more than 8 losses cut the run-time
     decode's outputs into chunks.  Encodes run the compiled gf_stream; decodes run gf_psyn
     (compiled syndromes + Gauss-Jordan) for the m >= 7 presets and gf_stream for the others,
-    never gf_apply; with psyn = 0 and stream_rc16 = 1, the run-time gf_stream decode in one
-    16-block unit.  Bit-exact vs the oracle in every decode layout, with as many losses as
+    never gf_apply; with psyn = 0, the run-time gf_stream decode (nibble-jump products) for
+    every preset.  The (5, 5) encode writes its parity through LDS-staged wide stores.  Bit-exact vs the oracle in every decode layout, with as many losses as
     the code allows (min(k, m)), with half of them and with one; grid 1: one workgroup
     streams every unit."""
     engine = tuned_engine
@@ -769,13 +778,9 @@ def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
         assert "gf_apply" not in fec.last_kernels()
 
 
-@pytest.mark.parametrize("wide", [0, 1])
-@pytest.mark.parametrize("jump", [2, 0])
-@pytest.mark.parametrize("pf", [1, 0])
-@pytest.mark.parametrize("depth", [5, 7])
 @pytest.mark.parametrize("grid", [1, 2, 0])
 @pytest.mark.parametrize("k,m", sorted(PSYN))
-def test_psyn_decode_patterns(tuned_engine, oracle, k, m, depth, grid, pf, jump, wide):
+def test_psyn_decode_patterns(tuned_engine, oracle, k, m, grid):
     """The preset decode (gf_psyn: syndromes of every parity row with the compiled code,
     Gauss-Jordan replayed on the data) on hand-built receive sets: no loss, 1 .. min(k, m)
     losses with first / scattered / last parity rows in any arrival order (blocks streamed
@@ -786,15 +791,11 @@ def test_psyn_decode_patterns(tuned_engine, oracle, k, m, depth, grid, pf, jump,
     the previous group's stores, up to 16 x 2 x min(k, m) of them)."""
     engine = tuned_engine
     engine.set_option("stream_grid", grid)
-    engine.set_option("psyn_depth", depth)
-    engine.set_option("psyn_pf", pf)
-    engine.set_option("psyn_jump", jump)
-    engine.set_option("wide_st", wide)
     bb = 1352
     rmax = min(k, m)
-    rng = np.random.default_rng(500 + 7 * k + m + depth + grid)
+    rng = np.random.default_rng(500 + 7 * k + m + grid)
     G = 26
-    data = synth.group_data(1901 + k + m + depth + grid, k, bb, G)
+    data = synth.group_data(1901 + k + m + grid, k, bb, G)
     p_or, _ = oracle.encode_batch(k, m, bb, data)
 
     def lose(lost, par):
@@ -837,6 +838,86 @@ def test_psyn_decode_patterns(tuned_engine, oracle, k, m, depth, grid, pf, jump,
     assert st.tolist() == [-3, -3]
     np.testing.assert_array_equal(rr, bad)
     np.testing.assert_array_equal(b, brecv)
+
+
+def test_psyn_grid_per_code(oracle):
+    """QuicR switches presets at run time (quic_connection.cc:822-966), so one context decodes
+    several codes.  Each code's gf_psyn grid is its own kernel's occupancy answer: decoding
+    (10, 20) first must not fix the grid of a later (10, 10) decode (one cache per kernel)."""
+    import torch
+    bb, G = 1352, 65536
+
+    def grid_of(eng, k, m):
+        rows, src = synth.loss_patterns(k, m, 1, 4, 17, shuffle=False)
+        rows = np.repeat(rows[:1], G, axis=0)
+        blocks = torch.zeros((G, k, bb), dtype=torch.uint8, device="cuda")
+        d_rows = torch.from_numpy(rows).cuda()
+        rec = torch.empty((G, min(k, m), bb), dtype=torch.uint8, device="cuda")
+        rec_rows = torch.empty((G, min(k, m)), dtype=torch.uint8, device="cuda")
+        st = torch.empty((G,), dtype=torch.int32, device="cuda")
+        eng.decode_recovered(k, m, bb, blocks, d_rows, rec, rec_rows, st)
+        torch.cuda.synchronize()
+        assert "gf_psyn_kernel" in fec.last_kernels()
+        return fec.last_grids()["gf_psyn_kernel"]
+
+    fresh = {}
+    for km in [(10, 10), (10, 20), (15, 15)]:
+        e = fec.FecEngine(0)
+        fresh[km] = grid_of(e, *km)
+        e.close()
+    e = fec.FecEngine(0)
+    for km in [(10, 20), (10, 10), (15, 15), (10, 10)]:
+        assert grid_of(e, *km) == fresh[km], km
+    e.close()
+    # the codes do differ in occupancy, so the check has teeth
+    assert fresh[(10, 10)] != fresh[(10, 20)]
+
+
+def test_workspace_eager_capture_other_stream():
+    """The decode workspace is one per context: an eager decode on stream A, then
+    a graph capture begun on A, then an eager decode on stream B.  B's prep must not overwrite
+    the tables A's eager decode is still reading: ws_end records an event after every eager
+    decode and ws_begin on B waits for it, whatever A does meanwhile.  Both decodes are
+    checked by their property (every lost data block restored)."""
+    import torch
+    k, m, bb = 32, 4, 1352
+    eng = fec.FecEngine(0)
+    ga, gb = 65536, 8192
+    eng.reserve(k, m, bb, ga)
+
+    def setup(G, lost, par, seed):
+        gen = torch.Generator(device="cuda").manual_seed(seed)
+        data = torch.randint(0, 256, (G, k, bb), dtype=torch.uint8, device="cuda", generator=gen)
+        parity = torch.empty((G, m, bb), dtype=torch.uint8, device="cuda")
+        eng.encode(k, m, bb, data, parity)
+        recv = data.clone()
+        rows = torch.arange(k, dtype=torch.uint8, device="cuda").repeat(G, 1)
+        for x, y in zip(lost, par):
+            recv[:, x] = parity[:, y]
+            rows[:, x] = k + y
+        rec = torch.full((G, m, bb), 0x5A, dtype=torch.uint8, device="cuda")
+        rr = torch.zeros((G, m), dtype=torch.uint8, device="cuda")
+        st = torch.full((G,), 7, dtype=torch.int32, device="cuda")
+        return data, recv, rows, rec, rr, st
+
+    A = setup(ga, [0, 1], [0, 1], 1)
+    B = setup(gb, [5, 9, 30], [3, 2, 1], 2)
+    C = setup(16, [2], [0], 3)                 # captured, never replayed
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    eng.decode_recovered(k, m, bb, A[1], A[2], A[3], A[4], A[5], stream=sa.cuda_stream)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=sa):
+        eng.decode_recovered(k, m, bb, C[1], C[2], C[3], C[4], C[5], stream=sa.cuda_stream)
+        eng.decode_recovered(k, m, bb, B[1], B[2], B[3], B[4], B[5], stream=sb.cuda_stream)
+    torch.cuda.synchronize()
+    for (data, recv, rows, rec, rr, st), lost in ((A, [0, 1]), (B, [5, 9, 30])):
+        assert bool((st == 0).all())
+        srt = sorted(lost)
+        assert bool((rr[:, :len(srt)] == torch.tensor(srt, dtype=torch.uint8, device="cuda")).all())
+        for j, x in enumerate(srt):
+            assert torch.equal(rec[:, j], data[:, x]), (x, j)
+    eng.close()
 
 
 # ------------------------------------------------- gf_bsyn (compiled (32, 4) decode, B/C)
@@ -905,8 +986,7 @@ D_KERNELS = {1: ("gf_dcol_kernel<encode,k128m16", "gf_dcol_kernel<decode,k128m16
              0: ("gf_apply_kernel<encode", "gf_apply_kernel<decode")}
 
 
-D_VARIANTS = [{"dcol": 1}, {"dcol": 1, "dcol_depth": 8}, {"dcol": 1, "dcol_rows": 8},
-              {"dcol": 0}]
+D_VARIANTS = [{"dcol": 1}, {"dcol": 1, "dcol_depth": 8}, {"dcol": 0}]
 
 
 @pytest.mark.parametrize("opts", D_VARIANTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
@@ -916,9 +996,8 @@ def test_tile_many_groups_per_workgroup(tuned_engine, oracle, grid, k, m, r, opt
     """Config D's kernels with the grid capped so one workgroup streams several groups back
     to back (the DMA prefetch crosses group / unit boundaries and the previous group's stores
     sit in the vmcnt count); every third group has no loss.  dcol = 1: gf_dcol (one wave
-    per column tile, units of (group, tile)) with its ring depth and rows-per-wave variants
-    (dcol_rows = 8: half tiles, no register prefetch, 4 waves per SIMD; encode only);
-    dcol = 0: the gf_apply fallback."""
+    per column tile, units of (group, tile)) at ring depths 6 and 8; dcol = 0: the gf_apply
+    fallback."""
     engine = tuned_engine
     for name, v in opts.items():
         engine.set_option(name, v)

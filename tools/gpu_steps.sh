@@ -14,11 +14,15 @@
 # Extra args use '+' for spaces: quick:B:--opt+ring_nt=0.  GPU_STEPS_DRY=1 prints the steps.
 export TMPDIR=/tmp
 specs=()
+tags=()
 for step in "$@"; do
   kind="${step%%:*}"; rest=""; [ "$step" != "$kind" ] && rest="${step#*:}"
   W="${rest%%:*}"; extra=""; [ "$rest" != "$W" ] && extra="${rest#*:}"
   extra="${extra//+/ }"
   tag=$(echo "$step" | tr -c 'A-Za-z0-9_\n' '_')
+  # a repeated step gets its own log: <tag>_2, <tag>_3, ...
+  n=1; base="$tag"; while [[ " ${tags[*]} " == *" $tag "* ]]; do n=$((n + 1)); tag="${base}_$n"; done
+  tags+=("$tag")
   quick="python bench.py --no-cpu-baseline --no-host --steps 10 --warmup 3"
   case "$kind" in
     tests)
