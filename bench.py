@@ -334,7 +334,36 @@ def packet_protection(eng, k, m, bb, data, parity, steps, stream):
     finally:
         lib.qfec_set_timing_events(None, None)
         ev.close()
+    # the same two group calls from host memory to host memory (pinned): the sender's and
+    # the receiver's whole per-packet paths including H2D / D2H (never `value`)
+    from quic_amd import fec
+    data_h = torch.empty(data.shape, dtype=torch.uint8, pin_memory=True)
+    data_h.copy_(data)
+    hdr_h = hdr.cpu().pin_memory()
+    hpkt = torch.empty((na, stride), dtype=torch.uint8, pin_memory=True)
+    hpkt_len = torch.empty(na, dtype=torch.int32, pin_memory=True)
+    hrcv_len = torch.empty(na, dtype=torch.int32, pin_memory=True)
+    hrec = torch.empty((G, rmax, bb), dtype=torch.uint8, pin_memory=True)
+    hrr = torch.empty((G, rmax), dtype=torch.uint8, pin_memory=True)
+    hst = torch.empty(G, dtype=torch.int32, pin_memory=True)
+    t_hs = t_ho = 0.0
+    g_lost_h = g_lost.cpu()
+    for i in range(steps + 1):
+        t0 = time.perf_counter()
+        fec.encode_seal_groups_host_into(eng, k, m, bb, data_h, hdr_h, hl, bb, hpkt, hpkt_len)
+        t1 = time.perf_counter()
+        hrcv_len.copy_(hpkt_len)
+        hrcv_len[g_lost_h] = -1
+        t2 = time.perf_counter()
+        fec.open_decode_host_into(eng, k, m, bb, hpkt, hrcv_len, hl, hrec, hrr, hst)
+        t3 = time.perf_counter()
+        if i:
+            t_hs += (t1 - t0) / steps
+            t_ho += (t3 - t2) / steps
     lost_i = torch.arange(G, device=dev) % k
+    host_ok = (bool((hpkt_len == hl + 12 + bb).all())
+               and bool((hst == 0).all())
+               and torch.equal(hrec[:, 0], data_h[torch.arange(G), lost_i.cpu()]))
     ok = (bool((plen == bb).all()) and torch.equal(plain[:, :bb], parity.view(n, bb))
           and torch.equal(pkt, pkt2) and bool((status == 0).all())
           and bool((rec_rows[:, 0] == lost_i.to(torch.uint8)).all())
@@ -354,6 +383,18 @@ def packet_protection(eng, k, m, bb, data, parity, steps, stream):
             "open_decode_ms": round(t["open_decode"], 5),
             "open_decode_GBps": round(all_bytes / t["open_decode"] / 1e6, 1),
             "round_trip_ok": ok,
+            "host": {
+                "encode_seal_groups_ms": round(t_hs * 1e3, 3),
+                "open_decode_ms": round(t_ho * 1e3, 3),
+                "GiBps": round(G * k * (bb - 2) / 2**30 / (t_hs + t_ho), 3),
+                "pcie_GBps": round((G * k * bb + na * (hl + stride + 4)
+                                    + na * (stride + 4) + G * rmax * (bb + 1) + 4 * G)
+                                   / (t_hs + t_ho) / 1e9, 2),
+                "ok": host_ok,
+                "note": "qfec_encode_seal_groups_batch_host then qfec_open_decode_batch_host "
+                        "on pinned host buffers (headers and data in, sealed packets out; "
+                        "packets in, recovered blocks out), wall clock per call, "
+                        "H2D/kernels/D2H pipelined in chunks"},
             "note": "kernel-bracketing events per call; one lane per packet (serial FNV "
                     "chain, six 22-bit limbs), DESIGN.md 6.2; open_decode loses data "
                     "packet g % k of group g"}

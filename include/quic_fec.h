@@ -223,6 +223,33 @@ QFEC_API int qfec_open_decode_batch(qfec_ctx *ctx, int k, int m, int block_bytes
                                     unsigned char *d_rows, int *d_open_len, unsigned char *d_rec,
                                     unsigned char *d_rec_rows, int *d_status, void *stream);
 
+/* Host-pointer variants of the two protected paths: the sender's and the receiver's per-packet
+ * work starting and ending in host memory (packets off and onto a socket), chunked and
+ * pipelined like qfec_*_batch_host (H2D, kernels and D2H of successive chunks overlap);
+ * synchronous; pass pinned memory for full PCIe speed.  Lengths, headers and packets are
+ * indexed by packet p = g*(k+m) + i as in the device calls; h_hdr may be NULL (no associated
+ * data: h_hdr_len NULL and hdr_len_all 0); h_pkt_len, h_pt_len and h_ad_len are int32 host
+ * arrays (NULL where the `_all` scalar applies, except h_pkt_len).  Row strides must be > 0.
+ *   qfec_encode_seal_groups_batch_host: data [G][k][bb] -> every packet of each group sealed,
+ *     h_pkt [G*(k+m)][pkt_stride], h_pkt_len [G*(k+m)] (qfec_encode_seal_groups_batch); the
+ *     bytes of a packet row past h_pkt_len[p] are unspecified (staging rows are copied whole);
+ *   qfec_open_decode_batch_host: wire packets -> h_rec [G][min(k,m)][bb], h_rec_rows,
+ *     h_status [G] (may be NULL) and h_open_len [G*(k+m)] (may be NULL)
+ *     (qfec_open_decode_batch). */
+QFEC_API int qfec_encode_seal_groups_batch_host(qfec_ctx *ctx, int k, int m, int block_bytes,
+                                                long long groups, const unsigned char *h_data,
+                                                const unsigned char *h_hdr, long long hdr_stride,
+                                                const int *h_hdr_len, int hdr_len_all,
+                                                const int *h_pt_len, int pt_len_all,
+                                                unsigned char *h_pkt, long long pkt_stride,
+                                                int *h_pkt_len);
+QFEC_API int qfec_open_decode_batch_host(qfec_ctx *ctx, int k, int m, int block_bytes,
+                                         long long groups, const unsigned char *h_pkt,
+                                         long long pkt_stride, const int *h_pkt_len,
+                                         const int *h_ad_len, int ad_len_all,
+                                         unsigned char *h_rec, unsigned char *h_rec_rows,
+                                         int *h_status, int *h_open_len);
+
 /* ---------------------------------------------------------------------------------
  * Support: the coefficient tables, a seeded synthetic workload, diagnostics.
  * ------------------------------------------------------------------------------- */

@@ -75,6 +75,14 @@ SIGNATURES = {
                                               ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p]),
+    "qfec_encode_seal_groups_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                          ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
+                                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                                          ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]),
+    "qfec_open_decode_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_longlong, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_void_p]),
     "qfec_cauchy_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "qfec_synth_fill": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_ulonglong, ctypes.c_ulonglong,
                                        ctypes.c_ulonglong, ctypes.c_void_p]),

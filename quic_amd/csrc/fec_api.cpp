@@ -496,7 +496,7 @@ int decode_recovered_impl(qfec_ctx* c, int k, int m, int bb, long long G,
 // at least the host_min_groups option's groups (512).
 // fn(g0, n, buf, phase): phase 0 enqueues the H2D, 1 the kernels, 2 the D2H.
 template <class F>
-int host_pipeline_body(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
+int host_pipeline_body(qfec_ctx* c, long long groups, size_t per_group, size_t slack, F&& fn) {
     if (!c->s_in) {
         QF_HIP(hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking));
         QF_HIP(hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
@@ -516,7 +516,7 @@ int host_pipeline_body(qfec_ctx* c, long long groups, size_t per_group, F&& fn) 
                                                   (long long)((2ull << 30) / per_group));
     const long long chunk =
         std::max<long long>(1, std::min<long long>(groups, std::max(by_bytes, floor_g)));
-    const size_t bytes = (size_t)chunk * per_group + 16;
+    const size_t bytes = (size_t)chunk * per_group + slack;
     for (int b = 0; b < qfec_ctx::NB; ++b) QF_HIP(c->pbuf[b].ensure(bytes));
     int i = 0;
     for (long long g0 = 0; g0 < groups; g0 += chunk, ++i) {
@@ -541,8 +541,12 @@ int host_pipeline_body(qfec_ctx* c, long long groups, size_t per_group, F&& fn) 
 // On any error, drain all three streams before returning, so no copy of an earlier chunk
 // still writes into the caller's host buffers after the call has returned.
 template <class F>
-int host_pipeline(qfec_ctx* c, long long groups, size_t per_group, F&& fn) {
-    const int r = host_pipeline_body(c, groups, per_group, fn);
+int host_pipeline(qfec_ctx* c, long long groups, size_t per_group, F&& fn, size_t slack = 16) {
+    // the kernels of every chunk run on the context stream: order them after the last eager
+    // use of the decode workspace, and the next use after them
+    int r = ws_begin(c, c->stream);
+    if (!r) r = host_pipeline_body(c, groups, per_group, slack, fn);
+    if (!r) r = ws_end(c, c->stream);
     if (r)
         for (hipStream_t s : {c->s_in, c->stream, c->s_out})
             if (s) (void)hipStreamSynchronize(s);
@@ -609,6 +613,38 @@ int resident_blocks(const void* kern, int threads, size_t lds) {
     return n;
 }
 }  // namespace qfec
+
+namespace {
+
+// NullDecrypter on every packet of each group, placement into the receive set, the
+// recovered-blocks decode, the unfilled-group status (qfec_open_decode_batch)
+int open_decode_impl(qfec_ctx* c, int k, int m, int bb, long long groups, const uint8_t* d_pkt,
+                     long long pkt_stride, const int* d_pkt_len, const int* d_ad_len,
+                     int ad_len_all, uint8_t* d_blocks, uint8_t* d_rows, int* d_open_len,
+                     uint8_t* d_rec, uint8_t* d_rec_rows, int* d_status, hipStream_t st) {
+    QF_HIP(qfec::launch_open_groups(c->pp_hash, k, m, bb, groups, d_pkt, pkt_stride,
+                                    (const int32_t*)d_pkt_len, (const int32_t*)d_ad_len,
+                                    ad_len_all, d_blocks, d_rows, (int32_t*)d_open_len, st));
+    int rc = decode_recovered_impl(c, k, m, bb, groups, d_blocks, d_rows, d_rec, d_rec_rows,
+                                   (int32_t*)d_status, st);
+    if (rc) return rc;
+    QF_HIP(qfec::launch_open_status(k, std::min(k, m), groups, d_rows, d_rec_rows,
+                                    (int32_t*)d_status, st));
+    return 0;
+}
+
+// Carves consecutive 256-byte aligned sub-buffers out of one staging buffer.
+struct Carve {
+    uint8_t* p;
+    uint8_t* take(size_t bytes) {
+        uint8_t* r = p;
+        p += (bytes + 255) & ~(size_t)255;
+        return r;
+    }
+};
+constexpr size_t kCarveSlack = 16 * 256;   // alignment padding of up to 16 sub-buffers
+
+}  // namespace
 
 // ======================================================================== C ABI
 extern "C" {
@@ -892,15 +928,12 @@ int qfec_open_decode_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
     std::lock_guard<std::mutex> lk(c->mu);
     if ((rc = set_device(c))) return rc;
     const hipStream_t st = pick(c, stream);
-    QF_HIP(qfec::launch_open_groups(c->pp_hash, k, m, bb, groups, d_pkt, pkt_stride, (const int32_t*)d_pkt_len,
-                                    (const int32_t*)d_ad_len, ad_len_all, d_blocks, d_rows,
-                                    (int32_t*)d_open_len, st));
-    if ((rc = decode_recovered_impl(c, k, m, bb, groups, d_blocks, d_rows, d_rec, d_rec_rows,
-                                    (int32_t*)d_status, st)))
+    if ((rc = ws_begin(c, st))) return rc;
+    if ((rc = open_decode_impl(c, k, m, bb, groups, d_pkt, pkt_stride, d_pkt_len, d_ad_len,
+                               ad_len_all, d_blocks, d_rows, d_open_len, d_rec, d_rec_rows,
+                               d_status, st)))
         return rc;
-    QF_HIP(qfec::launch_open_status(k, std::min(k, m), groups, d_rows, d_rec_rows,
-                                    (int32_t*)d_status, st));
-    return 0;
+    return ws_end(c, st);
 }
 
 int qfec_decode_batch_recovered_host(qfec_ctx* c, int k, int m, int bb, long long groups,
@@ -943,6 +976,135 @@ int qfec_decode_batch_recovered_host(qfec_ctx* c, int k, int m, int bb, long lon
         }
         return 0;
     });
+}
+
+// Sender, host memory to host memory: data blocks and packet headers in, every sealed packet
+// of each group out (the parity never leaves the device).  Chunked and pipelined as the
+// other host batches: H2D of chunk i + 1 and D2H of chunk i - 1 overlap chunk i's encode and
+// seal.
+int qfec_encode_seal_groups_batch_host(qfec_ctx* c, int k, int m, int bb, long long groups,
+                                       const unsigned char* h_data, const unsigned char* h_hdr,
+                                       long long hdr_stride, const int* h_hdr_len,
+                                       int hdr_len_all, const int* h_pt_len, int pt_len_all,
+                                       unsigned char* h_pkt, long long pkt_stride,
+                                       int* h_pkt_len) {
+    const unsigned char* dummy = (const unsigned char*)16;   // non-null for the argument check
+    int rc = seal_groups_args(c, k, m, bb, groups, h_data, dummy, h_hdr, hdr_stride, h_hdr_len,
+                              hdr_len_all, h_pt_len, pt_len_all, h_pkt, pkt_stride, h_pkt_len);
+    if (rc) return rc;
+    if (groups == 0) return 0;
+    if (hdr_stride <= 0 && h_hdr) return fail(-2, "host headers need a row stride > 0");
+    if (pkt_stride <= 0) return fail(-2, "host packets need a row stride > 0");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    const long long np = k + m;                        // packets per group
+    const size_t in_g = (size_t)k * bb, par_g = (size_t)m * bb;
+    const size_t hdr_g = h_hdr ? (size_t)np * hdr_stride : 0;
+    const size_t pkt_g = (size_t)np * pkt_stride;
+    const size_t len_g = (size_t)np * sizeof(int32_t);
+    const size_t per = in_g + par_g + hdr_g + pkt_g + len_g * (1 + (h_hdr_len ? 1 : 0) + (h_pt_len ? 1 : 0));
+    int result = 0;
+    rc = host_pipeline(c, groups, per, [&](long long g0, long long n, uint8_t* buf,
+                                           int phase) -> int {
+        Carve cv{buf};
+        uint8_t* dd = cv.take((size_t)n * in_g);
+        uint8_t* dp = cv.take((size_t)n * par_g);
+        uint8_t* dh = h_hdr ? cv.take((size_t)n * hdr_g) : nullptr;
+        uint8_t* dk = cv.take((size_t)n * pkt_g);
+        int32_t* dkl = (int32_t*)cv.take((size_t)n * len_g);
+        int32_t* dhl = h_hdr_len ? (int32_t*)cv.take((size_t)n * len_g) : nullptr;
+        int32_t* dpl = h_pt_len ? (int32_t*)cv.take((size_t)n * len_g) : nullptr;
+        const size_t p0 = (size_t)g0 * np, pn = (size_t)n * np;
+        if (phase == 0) {
+            QF_HIP(hipMemcpyAsync(dd, h_data + (size_t)g0 * in_g, (size_t)n * in_g,
+                                  hipMemcpyHostToDevice, c->s_in));
+            if (dh)
+                QF_HIP(hipMemcpyAsync(dh, h_hdr + p0 * hdr_stride, pn * hdr_stride,
+                                      hipMemcpyHostToDevice, c->s_in));
+            if (dhl)
+                QF_HIP(hipMemcpyAsync(dhl, h_hdr_len + p0, pn * sizeof(int32_t),
+                                      hipMemcpyHostToDevice, c->s_in));
+            if (dpl)
+                QF_HIP(hipMemcpyAsync(dpl, h_pt_len + p0, pn * sizeof(int32_t),
+                                      hipMemcpyHostToDevice, c->s_in));
+        } else if (phase == 1) {
+            const int r = encode_impl(c, k, m, bb, n, dd, dp, c->stream);
+            if (r < -1) return r;
+            if (r) result = r;
+            QF_HIP(qfec::launch_null_seal_groups(c->pp_hash, k, m, bb, n, dd, dp, dh,
+                                                 dh ? hdr_stride : 0, dhl, dh ? hdr_len_all : 0,
+                                                 dpl, pt_len_all, dk, pkt_stride, dkl, c->stream));
+        } else {
+            QF_HIP(hipMemcpyAsync(h_pkt + p0 * pkt_stride, dk, pn * pkt_stride,
+                                  hipMemcpyDeviceToHost, c->s_out));
+            QF_HIP(hipMemcpyAsync(h_pkt_len + p0, dkl, pn * sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, c->s_out));
+        }
+        return 0;
+    }, kCarveSlack);
+    return rc ? rc : result;
+}
+
+// Receiver, host memory to host memory: wire packets in, the recovered blocks (and, if asked,
+// each packet's open length) out.  Chunked and pipelined as the other host batches.
+int qfec_open_decode_batch_host(qfec_ctx* c, int k, int m, int bb, long long groups,
+                                const unsigned char* h_pkt, long long pkt_stride,
+                                const int* h_pkt_len, const int* h_ad_len, int ad_len_all,
+                                unsigned char* h_rec, unsigned char* h_rec_rows, int* h_status,
+                                int* h_open_len) {
+    int rc = check_common(c, k, m, bb, groups);
+    if (rc) return rc;
+    if (k + m > 255) return fail(-2, "k + m > 255 (row tag 255 marks an unfilled slot)");
+    if (groups == 0) return 0;
+    if (!h_pkt || !h_pkt_len || !h_rec || !h_rec_rows) return fail(-2, "null buffer");
+    if (pkt_stride <= 0) return fail(-2, "bad pkt_stride");
+    if (!h_ad_len && ad_len_all < 0) return fail(-2, "bad ad_len_all");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    const long long np = k + m;
+    const int rmax = std::min(k, m);
+    const size_t pkt_g = (size_t)np * pkt_stride, len_g = (size_t)np * sizeof(int32_t);
+    const size_t blk_g = (size_t)k * bb, rec_g = (size_t)rmax * bb;
+    const size_t per = pkt_g + len_g * (2 + (h_ad_len ? 1 : 0)) + blk_g + k + rec_g + rmax +
+                       sizeof(int32_t);
+    return host_pipeline(c, groups, per, [&](long long g0, long long n, uint8_t* buf,
+                                             int phase) -> int {
+        Carve cv{buf};
+        uint8_t* dk = cv.take((size_t)n * pkt_g);
+        int32_t* dkl = (int32_t*)cv.take((size_t)n * len_g);
+        int32_t* dal = h_ad_len ? (int32_t*)cv.take((size_t)n * len_g) : nullptr;
+        int32_t* dol = (int32_t*)cv.take((size_t)n * len_g);
+        uint8_t* db = cv.take((size_t)n * blk_g);
+        uint8_t* dr = cv.take((size_t)n * k);
+        uint8_t* dre = cv.take((size_t)n * rec_g);
+        uint8_t* drr = cv.take((size_t)n * rmax);
+        int32_t* ds = (int32_t*)cv.take((size_t)n * sizeof(int32_t));
+        const size_t p0 = (size_t)g0 * np, pn = (size_t)n * np;
+        if (phase == 0) {
+            QF_HIP(hipMemcpyAsync(dk, h_pkt + p0 * pkt_stride, pn * pkt_stride,
+                                  hipMemcpyHostToDevice, c->s_in));
+            QF_HIP(hipMemcpyAsync(dkl, h_pkt_len + p0, pn * sizeof(int32_t),
+                                  hipMemcpyHostToDevice, c->s_in));
+            if (dal)
+                QF_HIP(hipMemcpyAsync(dal, h_ad_len + p0, pn * sizeof(int32_t),
+                                      hipMemcpyHostToDevice, c->s_in));
+        } else if (phase == 1) {
+            return open_decode_impl(c, k, m, bb, n, dk, pkt_stride, dkl, dal, ad_len_all, db, dr,
+                                    dol, dre, drr, ds, c->stream);
+        } else {
+            QF_HIP(hipMemcpyAsync(h_rec + (size_t)g0 * rec_g, dre, (size_t)n * rec_g,
+                                  hipMemcpyDeviceToHost, c->s_out));
+            QF_HIP(hipMemcpyAsync(h_rec_rows + (size_t)g0 * rmax, drr, (size_t)n * rmax,
+                                  hipMemcpyDeviceToHost, c->s_out));
+            if (h_status)
+                QF_HIP(hipMemcpyAsync(h_status + g0, ds, (size_t)n * sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, c->s_out));
+            if (h_open_len)
+                QF_HIP(hipMemcpyAsync(h_open_len + p0, dol, pn * sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, c->s_out));
+        }
+        return 0;
+    }, kCarveSlack);
 }
 
 int qfec_encode_batch_host(qfec_ctx* c, int k, int m, int bb, long long groups,

@@ -326,6 +326,46 @@ def decode_host_into(engine, k, m, block_bytes, blocks_h, rows_h, status_h=None)
     return rc
 
 
+def _hlens(lens):
+    """(host array pointer, scalar) for a per-packet length argument of a host call: an int32
+    CPU tensor, or an int meaning the same length for every packet."""
+    if isinstance(lens, int):
+        return None, lens
+    return _hptr(lens), 0
+
+
+def encode_seal_groups_host_into(engine, k, m, block_bytes, data_h, hdr_h, hdr_len, pt_len,
+                                 pkt_h, pkt_len_h):
+    """Sender, host to host (qfec_encode_seal_groups_batch_host): data [G][k][bb] and
+    headers hdr [G*(k+m)][hdr_stride] (or None) -> every packet sealed into pkt
+    [G*(k+m)][pkt_stride], pkt_len int32 [G*(k+m)].  Returns 0 / -1."""
+    h, h_all = _hlens(hdr_len)
+    p, p_all = _hlens(pt_len)
+    rc = engine.lib.qfec_encode_seal_groups_batch_host(
+        engine._h, k, m, block_bytes, data_h.shape[0], _hptr(data_h),
+        None if hdr_h is None else _hptr(hdr_h), 0 if hdr_h is None else hdr_h.stride(0), h,
+        h_all, p, p_all, _hptr(pkt_h), pkt_h.stride(0), _hptr(pkt_len_h))
+    if rc < -1:
+        raise FecError(rc, "qfec_encode_seal_groups_batch_host")
+    return rc
+
+
+def open_decode_host_into(engine, k, m, block_bytes, pkt_h, pkt_len_h, ad_len, rec_h,
+                          rec_rows_h, status_h=None, open_len_h=None):
+    """Receiver, host to host (qfec_open_decode_batch_host): wire packets pkt
+    [G*(k+m)][stride], pkt_len int32 (< 0: not received) -> rec [G][min(k,m)][bb],
+    rec_rows, status [G], open_len [G*(k+m)]."""
+    a, a_all = _hlens(ad_len)
+    rc = engine.lib.qfec_open_decode_batch_host(
+        engine._h, k, m, block_bytes, rec_h.shape[0], _hptr(pkt_h), pkt_h.stride(0),
+        _hptr(pkt_len_h), a, a_all, _hptr(rec_h), _hptr(rec_rows_h),
+        None if status_h is None else _hptr(status_h),
+        None if open_len_h is None else _hptr(open_len_h))
+    if rc:
+        raise FecError(rc, "qfec_open_decode_batch_host")
+    return rc
+
+
 def decode_recovered_host_into(engine, k, m, block_bytes, blocks_h, rows_h, rec_h, rec_rows_h,
                                status_h=None):
     """Host-pointer decode returning only the recovered blocks (CPU tensors)."""

@@ -318,6 +318,62 @@ def test_open_decode_vs_oracle(pp_engine, oracle, k, m, G, bb):
                 assert np.array_equal(got_rec[g, j], data[g, rec_rows[g, j]])
 
 
+@pytest.mark.parametrize("chunk", [0, 1], ids=["one_chunk", "many_chunks"])
+@pytest.mark.parametrize("k,m,G", [(10, 1, 40), (5, 5, 30), (32, 4, 12), (10, 20, 9)])
+def test_host_protected_paths_vs_oracle(oracle, k, m, G, chunk):
+    """The sender's and the receiver's per-packet paths from host memory to host memory
+    (qfec_encode_seal_groups_batch_host, qfec_open_decode_batch_host), bit-exact with the
+    oracle's NullEncrypter / NullDecrypter and decode; many_chunks: one group per pipelined
+    chunk (host_chunk_mb = host_min_groups = 1), so H2D, kernels and D2H of successive
+    chunks overlap across the staging buffers."""
+    import torch
+    from quic_amd import fec
+    eng = fec.FecEngine(0)
+    if chunk:
+        eng.set_option("host_chunk_mb", 1)
+        eng.set_option("host_min_groups", 1)
+    bb = 1352
+    rng = np.random.default_rng(k * 31 + m + G + chunk)
+    per, n = k + m, G * (k + m)
+    data, parity, pt_len, hdr, hdr_len, exp, eres = _group_packets(oracle, k, m, bb, G, rng)
+    # sender: data + headers in host memory -> every sealed packet in host memory
+    h_pkt = torch.zeros((n, exp.shape[1]), dtype=torch.uint8).pin_memory()
+    h_len = torch.full((n,), 7, dtype=torch.int32).pin_memory()
+    rc = fec.encode_seal_groups_host_into(eng, k, m, bb, torch.from_numpy(data).pin_memory(),
+                                          torch.from_numpy(hdr).pin_memory(),
+                                          torch.from_numpy(hdr_len), torch.from_numpy(pt_len),
+                                          h_pkt, h_len)
+    assert rc == 0
+    assert np.array_equal(h_len.numpy(), eres)
+    got = h_pkt.numpy()
+    for p in range(n):                       # a row's bytes past its length are unspecified
+        assert np.array_equal(got[p, :eres[p]], exp[p, :eres[p]]), p
+    # receiver: lost and tampered packets, one unrecoverable group
+    pkt, pkt_len = exp.copy(), eres.copy()
+    lost = rng.random(n) < 0.3 * m / per
+    pkt_len[lost] = -1
+    for p in np.flatnonzero(~lost & (rng.random(n) < 0.1 * m / per))[:3]:
+        pkt[p, hdr_len[p] + 3] ^= 0x10
+    pkt_len[0] = -1
+    pkt_len[k:per] = -1
+    open_len, blocks, rows, ok, rec, rec_rows, status = _expected_open_decode(
+        oracle, k, m, bb, G, pkt, pkt_len, hdr_len)
+    rmax = min(k, m)
+    h_rec = torch.zeros((G, rmax, bb), dtype=torch.uint8).pin_memory()
+    h_rr = torch.zeros((G, rmax), dtype=torch.uint8).pin_memory()
+    h_st = torch.full((G,), 99, dtype=torch.int32).pin_memory()
+    h_ol = torch.zeros(n, dtype=torch.int32).pin_memory()
+    fec.open_decode_host_into(eng, k, m, bb, torch.from_numpy(pkt).pin_memory(),
+                              torch.from_numpy(pkt_len).pin_memory(), torch.from_numpy(hdr_len),
+                              h_rec, h_rr, h_st, h_ol)
+    assert np.array_equal(h_ol.numpy(), open_len)
+    assert np.array_equal(h_st.numpy(), status)
+    assert np.array_equal(h_rr.numpy()[ok], rec_rows[ok])
+    used = rec_rows != 255
+    assert np.array_equal(h_rec.numpy()[used], rec[used])
+    eng.close()
+
+
 def test_open_decode_full_size_a_shape(engine):
     """BASELINE config A's shape, 65,536 groups of (10 + 1) x 1352 B: every packet of every
     group sealed in one launch after the encode, one random packet per group lost, then
