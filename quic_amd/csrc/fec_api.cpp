@@ -147,7 +147,6 @@ struct qfec_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     qfec::Tune tune;
-    int pp_hash = 0;   // packet protection's FNV chain: 0 six 22-bit limbs, 1 64-bit halves
     // The decode workspace (dcoef, dslots, dnout, dscratch) is one per context.  Calls may
     // enqueue on any stream: every eager use records ws_ev after its kernels, and a use on
     // another stream waits for it, so uses of the workspace are ordered across streams
@@ -622,7 +621,7 @@ int open_decode_impl(qfec_ctx* c, int k, int m, int bb, long long groups, const 
                      long long pkt_stride, const int* d_pkt_len, const int* d_ad_len,
                      int ad_len_all, uint8_t* d_blocks, uint8_t* d_rows, int* d_open_len,
                      uint8_t* d_rec, uint8_t* d_rec_rows, int* d_status, hipStream_t st) {
-    QF_HIP(qfec::launch_open_groups(c->pp_hash, k, m, bb, groups, d_pkt, pkt_stride,
+    QF_HIP(qfec::launch_open_groups(k, m, bb, groups, d_pkt, pkt_stride,
                                     (const int32_t*)d_pkt_len, (const int32_t*)d_ad_len,
                                     ad_len_all, d_blocks, d_rows, (int32_t*)d_open_len, st));
     int rc = decode_recovered_impl(c, k, m, bb, groups, d_blocks, d_rows, d_rec, d_rec_rows,
@@ -684,7 +683,6 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
         {"host_min_groups", &t.host_min_groups, 1, 1 << 20},
-        {"pp_hash", &c->pp_hash, 0, 1},
     };
     for (const Opt& o : opts) {
         if (strcmp(o.n, name) != 0) continue;
@@ -709,7 +707,6 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"psyn", t.psyn},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb}, {"host_min_groups", t.host_min_groups},
-        {"pp_hash", c->pp_hash},
     };
     for (const auto& o : opts)
         if (strcmp(o.first, name) == 0) { *value = o.second; return 0; }
@@ -810,7 +807,7 @@ int qfec_null_seal_batch(qfec_ctx* c, long long n, const unsigned char* d_ad, lo
     std::lock_guard<std::mutex> lk(c->mu);
     int rc;
     if ((rc = set_device(c))) return rc;
-    QF_HIP(qfec::launch_null_seal_h(c->pp_hash, n, d_ad, ad_stride, (const int32_t*)d_ad_len, ad_len_all, d_pt,
+    QF_HIP(qfec::launch_null_seal_h(n, d_ad, ad_stride, (const int32_t*)d_ad_len, ad_len_all, d_pt,
                                   pt_stride, (const int32_t*)d_pt_len, pt_len_all, d_out,
                                   out_stride, (int32_t*)d_out_len, pick(c, stream)));
     return 0;
@@ -827,7 +824,7 @@ int qfec_null_open_batch(qfec_ctx* c, long long n, const unsigned char* d_pkt, l
     std::lock_guard<std::mutex> lk(c->mu);
     int rc;
     if ((rc = set_device(c))) return rc;
-    QF_HIP(qfec::launch_null_open_h(c->pp_hash, n, d_pkt, pkt_stride, (const int32_t*)d_pkt_len, pkt_len_all,
+    QF_HIP(qfec::launch_null_open_h(n, d_pkt, pkt_stride, (const int32_t*)d_pkt_len, pkt_len_all,
                                   (const int32_t*)d_ad_len, ad_len_all, d_out, out_stride,
                                   (int32_t*)d_out_len, pick(c, stream)));
     return 0;
@@ -850,7 +847,7 @@ int qfec_encode_seal_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
     // SerializeFec (quic_packet_creator.cc:935-957): parity packets from the group's encode,
     // each sealed with its packet header as the associated data; packet (g, i) = g * m + i
     if ((rc = encode_impl(c, k, m, bb, groups, d_data, d_parity, st))) return rc;
-    QF_HIP(qfec::launch_null_seal_h(c->pp_hash, groups * m, d_hdr, hdr_stride, (const int32_t*)d_hdr_len,
+    QF_HIP(qfec::launch_null_seal_h(groups * m, d_hdr, hdr_stride, (const int32_t*)d_hdr_len,
                                   hdr_len_all, d_parity, bb, nullptr, bb, d_pkt, pkt_stride,
                                   (int32_t*)d_pkt_len, st));
     return 0;
@@ -884,7 +881,7 @@ int qfec_seal_groups_batch(qfec_ctx* c, int k, int m, int bb, long long groups,
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(c->mu);
     if ((rc = set_device(c))) return rc;
-    QF_HIP(qfec::launch_null_seal_groups(c->pp_hash, k, m, bb, groups, d_data, d_parity, d_hdr, hdr_stride,
+    QF_HIP(qfec::launch_null_seal_groups(k, m, bb, groups, d_data, d_parity, d_hdr, hdr_stride,
                                          (const int32_t*)d_hdr_len, hdr_len_all,
                                          (const int32_t*)d_pt_len, pt_len_all, d_pkt, pkt_stride,
                                          (int32_t*)d_pkt_len, pick(c, stream)));
@@ -904,7 +901,7 @@ int qfec_encode_seal_groups_batch(qfec_ctx* c, int k, int m, int bb, long long g
     if ((rc = set_device(c))) return rc;
     const hipStream_t st = pick(c, stream);
     if ((rc = encode_impl(c, k, m, bb, groups, d_data, d_parity, st))) return rc;
-    QF_HIP(qfec::launch_null_seal_groups(c->pp_hash, k, m, bb, groups, d_data, d_parity, d_hdr, hdr_stride,
+    QF_HIP(qfec::launch_null_seal_groups(k, m, bb, groups, d_data, d_parity, d_hdr, hdr_stride,
                                          (const int32_t*)d_hdr_len, hdr_len_all,
                                          (const int32_t*)d_pt_len, pt_len_all, d_pkt, pkt_stride,
                                          (int32_t*)d_pkt_len, st));
@@ -1031,7 +1028,7 @@ int qfec_encode_seal_groups_batch_host(qfec_ctx* c, int k, int m, int bb, long l
             const int r = encode_impl(c, k, m, bb, n, dd, dp, c->stream);
             if (r < -1) return r;
             if (r) result = r;
-            QF_HIP(qfec::launch_null_seal_groups(c->pp_hash, k, m, bb, n, dd, dp, dh,
+            QF_HIP(qfec::launch_null_seal_groups(k, m, bb, n, dd, dp, dh,
                                                  dh ? hdr_stride : 0, dhl, dh ? hdr_len_all : 0,
                                                  dpl, pt_len_all, dk, pkt_stride, dkl, c->stream));
         } else {

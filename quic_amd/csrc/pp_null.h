@@ -8,14 +8,12 @@
 
 namespace qfec {
 
-// form (every launcher here): the FNV-1a-128 chain, 0 = six 22-bit limbs, 1 = 64-bit halves
-// (context option "pp_hash"; pp_null.hip)
-hipError_t launch_null_seal_h(int form, long long n, const uint8_t* ad, long long ad_stride,
+hipError_t launch_null_seal_h(long long n, const uint8_t* ad, long long ad_stride,
                               const int32_t* ad_len, int ad_all, const uint8_t* pt,
                               long long pt_stride, const int32_t* pt_len, int pt_all,
                               uint8_t* out, long long out_stride, int32_t* out_len,
                               hipStream_t st);
-hipError_t launch_null_open_h(int form, long long n, const uint8_t* pkt, long long pkt_stride,
+hipError_t launch_null_open_h(long long n, const uint8_t* pkt, long long pkt_stride,
                               const int32_t* pkt_len, int pkt_all, const int32_t* ad_len,
                               int ad_all, uint8_t* out, long long out_stride, int32_t* out_len,
                               hipStream_t st);
@@ -24,7 +22,7 @@ hipError_t launch_null_open_h(int form, long long n, const uint8_t* pkt, long lo
 // i < k, parity block (g, i - k) otherwise (rows of bb bytes), PT length pt_len[p] (or
 // pt_all), wire packet at out + p * out_stride (quic_packet_creator.cc:733-736 seals every
 // data packet, :948-953 every FEC packet).
-hipError_t launch_null_seal_groups(int form, int k, int m, int bb, long long groups, const uint8_t* data,
+hipError_t launch_null_seal_groups(int k, int m, int bb, long long groups, const uint8_t* data,
                                    const uint8_t* parity, const uint8_t* hdr,
                                    long long hdr_stride, const int32_t* hdr_len, int hdr_all,
                                    const int32_t* pt_len, int pt_all, uint8_t* out,
@@ -35,7 +33,7 @@ hipError_t launch_null_seal_groups(int form, int k, int m, int bb, long long gro
 // (not received, malformed, longer than bb, or tag mismatch).  Then one wave per group builds
 // rows[g][*] (data row i where packet i opened, else the next opened parity packet, ascending,
 // whose plaintext it copies into the hole; 255 when none is left) for the decode.
-hipError_t launch_open_groups(int form, int k, int m, int bb, long long groups, const uint8_t* pkt,
+hipError_t launch_open_groups(int k, int m, int bb, long long groups, const uint8_t* pkt,
                               long long pkt_stride, const int32_t* pkt_len,
                               const int32_t* ad_len, int ad_all, uint8_t* blocks,
                               uint8_t* rows, int32_t* open_len, hipStream_t st);

@@ -21,7 +21,7 @@
 // 24-bit multiplies (v_mul_u32_u24; a limb stays below 2^24, its product below 2^32), each
 // limb keeps its low 22 bits and passes the rest up one limb, and h << 88 is two limb adds
 // (88 = 4 * 22): about 25 full-rate VALU operations per byte, with six independent lanes of
-// work, against seven quarter-rate 32-bit multiplies for the plain 64-bit-halves form.  The
+// work, against seven quarter-rate 32-bit multiplies for a 64-bit-halves form.  The
 // low limb is always exact (nothing carries into it), so the byte XOR is exact too; the
 // limbs are normalised once, for the tag.  Bound: the VALU.
 //
@@ -87,33 +87,6 @@ struct Fnv {
         const uint64_t lo = (uint64_t)n[0] | ((uint64_t)n[1] << 22) | ((uint64_t)n[2] << 44);
         const uint64_t hi = ((uint64_t)n[2] >> 20) | ((uint64_t)n[3] << 2) |
                             ((uint64_t)n[4] << 24) | ((uint64_t)n[5] << 46);
-        t0 = (uint32_t)lo;
-        t1 = (uint32_t)(lo >> 32);
-        t2 = (uint32_t)hi;
-    }
-};
-
-// The plain form (pp_hash = 1): 64-bit halves, h * (2^88 + 315) = h * 315 + (h << 88), i.e.
-// lo' = lo * 315, hi' = hi * 315 + mulhi(lo, 315) + (lo << 24) (64-bit multiply-adds).
-struct Fnv64 {
-    uint64_t lo, hi;
-    __device__ __forceinline__ void init() {
-        hi = 7809847782465536322ull;
-        lo = 7113472399480571277ull;
-    }
-    __device__ __forceinline__ void byte(uint32_t b) {
-        lo ^= b;
-        const uint64_t nhi = hi * 315u + __umul64hi(lo, 315u) + (lo << 24);
-        lo *= 315u;
-        hi = nhi;
-    }
-    __device__ __forceinline__ void word(uint32_t w) {
-        byte(w & 0xFFu);
-        byte((w >> 8) & 0xFFu);
-        byte((w >> 16) & 0xFFu);
-        byte(w >> 24);
-    }
-    __device__ __forceinline__ void tag(uint32_t& t0, uint32_t& t1, uint32_t& t2) const {
         t0 = (uint32_t)lo;
         t1 = (uint32_t)(lo >> 32);
         t2 = (uint32_t)hi;
@@ -296,6 +269,176 @@ __device__ __forceinline__ int len_of(const int32_t* a, int all, long long i) {
     return a ? a[i] : all;
 }
 
+// ------------------------------------------------------------------ wave-tiled stream
+// The packets of a wave are streamed through an 8 KB LDS tile in 128-byte windows, so that
+// both the loads and the stores are coalesced: one wave instruction moves 8 packets x 128
+// contiguous bytes (8 lanes per packet, 16 bytes each) instead of 64 packets x 16 bytes, which
+// touched 64 cache lines per instruction and cost 1.4x the reads (L2 re-fetches) and 1.55x
+// the writes (partial lines) of the one-lane-per-packet streamer (profiles/r05/pp/).  Each lane
+// still owns its packet's serial FNV chain.
+//   window w of packet q: source chunks 8w .. 8w + 7 (16 bytes each, from its 16-byte aligned
+//   start); the tile row of packet q is 128 bytes at q * 128, chunk c at slot c ^ (q & 7) (an
+//   XOR swizzle: lanes reading their rows at one chunk index hit distinct banks).
+//   1. loads: 8 global_load_lds_dwordx4 (instruction j: packets 8j .. 8j + 7, lane = 8 (q % 8)
+//      + slot), each lane's address from its packet's lane by ds_bpermute;
+//   2. lane q reads its 8 chunks, hashes the valid bytes, and writes each FULL 16-byte output
+//      line (realigned to the output's phase, zeros past the source) back into the slot of the
+//      chunk it just consumed;
+//   3. stores: 8 global_store_dwordx4 in the same shape (full lines only).
+// The partial output lines at the two ends (< 16 bytes each) are written byte by byte.
+// Measured variants: 64-byte windows double-buffered, and two packets
+// per lane (two interleaved chains) with 64-byte windows, were both slower.
+constexpr int kTileBytes = 64 * 128;   // one wave's tile
+constexpr int kTilePackets = 64;       // packets per wave (one per lane)
+
+__device__ __forceinline__ uint32_t bperm(uint32_t v, int src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, int src_lane) {
+    return (uint64_t)bperm((uint32_t)v, src_lane) | ((uint64_t)bperm((uint32_t)(v >> 32), src_lane) << 32);
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+// A[idx] for a per-lane idx in 0..7
+__device__ __forceinline__ uint32_t pick8(const uint32_t (&A)[8], int idx) {
+    const uint32_t a0 = (idx & 1) ? A[1] : A[0], a1 = (idx & 1) ? A[3] : A[2];
+    const uint32_t a2 = (idx & 1) ? A[5] : A[4], a3 = (idx & 1) ? A[7] : A[6];
+    const uint32_t b0 = (idx & 2) ? a1 : a0, b1 = (idx & 2) ? a3 : a2;
+    return (idx & 4) ? b1 : b0;
+}
+
+// Hash pl source bytes at src into h and write them to dst, followed by zeros up to olen
+// bytes (olen == 0: hash only).  Called by every lane of the wave together (wave-uniform
+// loop); a lane with pl == 0 and olen == 0 only takes part.  tile: this wave's kTileBytes of
+// LDS.  Every memory access of the routine is complete when it returns.
+template <class H>
+__device__ void tile_stream(H& h, const uint8_t* src, int pl, uint8_t* dst, int olen,
+                            uint8_t* tile) {
+    const int lane = (int)__lane_id();
+    const uintptr_t sp = (uintptr_t)src;
+    const int hoff = pl > 0 ? (int)(sp & 15u) : 0;
+    const uint64_t s16 = (uint64_t)(sp - hoff);
+    const int cmax = pl > 0 ? (hoff + pl - 1) >> 4 : -1;   // last chunk holding a source byte
+    const int send = hoff + pl;                             // source end, chunk coordinates
+    // output: stream byte x goes to D + x, D = dst - hoff; 16-byte lines from A0 = D rounded
+    // down; the full lines jf .. jl lie inside [dst, dst + olen)
+    const uint64_t D = (uint64_t)(uintptr_t)dst - (uint64_t)hoff;
+    const int e = (int)(D & 15u);
+    const uint64_t A0 = D - (uint64_t)e;
+    int jf = 0, jl = -1;
+    if (olen > 0) {
+        jf = (int)(((uint64_t)(uintptr_t)dst - A0 + 15u) >> 4);
+        jl = (int)(((uint64_t)(uintptr_t)dst + (uint64_t)olen - A0) >> 4) - 1;
+    }
+    const int last = max(cmax, jl);
+    const int nwin_l = last >= 0 ? (last >> 3) + 1 : 0;
+    const int nwin = wave_max(nwin_l);
+    // line g = stream bytes [16 g - e, 16 g - e + 16): from (previous chunk, this chunk)
+    const int mi = (16 - e) >> 2, ri = (16 - e) & 3;
+    uint32_t P[4] = {0u, 0u, 0u, 0u};
+    const int lq = lane >> 3, pos = lane & 7;
+    const int rowoff = lane * 128, sw = lane & 7;
+    const uint32_t tb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)tile;
+#pragma unroll 1
+    for (int w = 0; w < nwin; ++w) {
+        // 1. coalesced loads: instruction j brings packets 8j .. 8j + 7
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int q = 8 * j + lq;
+            const uint64_t qs = bperm64(s16, q);
+            const int qc = (int)bperm((uint32_t)cmax, q);
+            const int cg = 8 * w + (pos ^ (q & 7));
+            if (cg <= qc)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(uintptr_t)(qs + 16u * (uint64_t)cg),
+                    (__attribute__((address_space(3))) void*)(tile + 1024 * j), 16, 0, 2);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        // 2. this lane's row: hash, and full output lines back into the tile
+        if (w < nwin_l) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int g = 8 * w + c;
+                const uint32_t a = tb + (uint32_t)(rowoff + ((c ^ sw) << 4));
+                uint32_t C[4] = {0u, 0u, 0u, 0u};
+                if (g <= cmax) {
+                    u32x4 v;
+                    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+                    C[0] = v.x, C[1] = v.y, C[2] = v.z, C[3] = v.w;
+                    const int x0 = 16 * g;
+                    if (x0 >= hoff && x0 + 16 <= send) {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) h.word(C[t]);
+                    } else {
+                        // a partial chunk: hash its valid bytes, zero the bytes past the source
+#pragma unroll 1
+                        for (int b = 0; b < 16; ++b) {
+                            const int x = x0 + b;
+                            if (x >= hoff && x < send) h.byte((C[b >> 2] >> (8 * (b & 3))) & 0xFFu);
+                        }
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int keep = min(max(send - (x0 + 4 * t), 0), 4);
+                            C[t] = keep >= 4 ? C[t] : keep <= 0 ? 0u : (C[t] & ((1u << (8 * keep)) - 1u));
+                        }
+                    }
+                }
+                if (g >= jf && g <= jl) {
+                    const uint32_t A[8] = {P[0], P[1], P[2], P[3], C[0], C[1], C[2], C[3]};
+                    u32x4 o;
+                    o.x = __builtin_amdgcn_alignbyte(pick8(A, min(mi + 1, 7)), pick8(A, mi), ri);
+                    o.y = __builtin_amdgcn_alignbyte(pick8(A, min(mi + 2, 7)), pick8(A, min(mi + 1, 7)), ri);
+                    o.z = __builtin_amdgcn_alignbyte(pick8(A, min(mi + 3, 7)), pick8(A, min(mi + 2, 7)), ri);
+                    o.w = __builtin_amdgcn_alignbyte(pick8(A, min(mi + 4, 7)), pick8(A, min(mi + 3, 7)), ri);
+                    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(o) : "memory");
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) P[t] = C[t];
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        // 3. coalesced stores of the full lines: instruction j, packets 8j .. 8j + 7
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int q = 8 * j + lq;
+            const int qf = (int)bperm((uint32_t)jf, q), ql = (int)bperm((uint32_t)jl, q);
+            const uint64_t qa = bperm64(A0, q);
+            const int g = 8 * w + pos;
+            if (g >= qf && g <= ql) {
+                const uint32_t a = tb + (uint32_t)(q * 128 + ((pos ^ (q & 7)) << 4));
+                u32x4 v;
+                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+                __builtin_nontemporal_store(v, (u32x4*)(uintptr_t)(qa + 16u * (uint64_t)g));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    // 4. the partial lines at both ends, byte by byte: at most 15 bytes each, or the whole
+    // output (< 32 bytes) when it has no full line; all loads in flight before the stores
+    if (olen > 0) {
+        const int nh = jl >= jf ? (int)(A0 + 16u * (uint64_t)jf - (uint64_t)(uintptr_t)dst) : olen;
+        const int tb0 = jl >= jf ? (int)(A0 + 16u * (uint64_t)(jl + 1) - (uint64_t)(uintptr_t)dst) : olen;
+        const int nt = olen - tb0;
+        uint32_t hv[32], tv[16];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) hv[i] = (i < nh && i < pl) ? src[i] : 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tv[i] = (i < nt && tb0 + i < pl) ? src[tb0 + i] : 0u;
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+            if (i < nh) dst[i] = (uint8_t)hv[i];
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (i < nt) dst[tb0 + i] = (uint8_t)tv[i];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // the 12 tag bytes at c against (t0, t1, t2)
 __device__ __forceinline__ bool tag_matches(const uint8_t* c, uint32_t t0, uint32_t t1,
                                             uint32_t t2) {
@@ -325,30 +468,35 @@ __device__ __forceinline__ const uint8_t* pt_row(const PtRows& r, long long p) {
     return i < r.ka ? r.a + (g * r.ka + i) * r.stride : r.b + (g * r.kb + (i - r.ka)) * r.stride;
 }
 
+// One wave seals 64 packets (one per lane): the AD through the lane's own streamer (a few
+// bytes), the plaintext through the wave's LDS tile (tile_stream), then the tag.
 template <class H>
-__global__ __launch_bounds__(kPPThreads) void null_seal_kernel(
+__global__ __launch_bounds__(64) void null_seal_kernel(
     long long n, const uint8_t* __restrict__ ad, long long ad_stride,
     const int32_t* __restrict__ ad_len, int ad_all, PtRows pr, const int32_t* __restrict__ pt_len,
     int pt_all, uint8_t* out, long long out_stride, int32_t* out_len) {
-    const long long i = (long long)blockIdx.x * kPPThreads + threadIdx.x;
-    if (i >= n) return;
-    const int al = len_of(ad_len, ad_all, i), pl = len_of(pt_len, pt_all, i);
-    // a row longer than its stride would read the next packet's bytes (or past the buffer for
-    // the last one): rejected like a packet that does not fit
-    const bool ok = al >= 0 && pl >= 0 && (ad_stride == 0 || al <= ad_stride) &&
-                    (pr.stride == 0 || pl <= pr.stride) && (long long)al + 12 + pl <= out_stride;
-    out_len[i] = ok ? al + 12 + pl : -1;
-    if (!ok) return;
-    uint8_t* o = out + i * out_stride;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const long long i = (long long)blockIdx.x * 64 + threadIdx.x;
+    bool ok = false;
+    int al = 0, pl = 0;
+    if (i < n) {
+        al = len_of(ad_len, ad_all, i);
+        pl = len_of(pt_len, pt_all, i);
+        // a row longer than its stride would read the next packet's bytes (or past the buffer
+        // for the last one): rejected like a packet that does not fit
+        ok = al >= 0 && pl >= 0 && (ad_stride == 0 || al <= ad_stride) &&
+             (pr.stride == 0 || pl <= pr.stride) && (long long)al + 12 + pl <= out_stride;
+        out_len[i] = ok ? al + 12 + pl : -1;
+    }
+    uint8_t* o = out + (ok ? i : 0) * out_stride;
     H h;
     h.init();
-    Sink s;
+    Sink s, t;
     s.begin(o);
-    span<true, true>(h, s, ad + i * ad_stride, al);
-    Sink t = s;   // AD's unstored tail bytes; the tag follows them once it is known
-    s.begin(o + al + 12);
-    span<true, true>(h, s, pt_row(pr, i), pl);
-    s.flush();
+    if (ok) span<true, true>(h, s, ad + i * ad_stride, al);
+    t = s;   // AD's unstored tail bytes; the tag follows them once it is known
+    tile_stream(h, ok ? pt_row(pr, i) : nullptr, ok ? pl : 0, o + al + 12, ok ? pl : 0, smem);
+    if (!ok) return;
     uint32_t t0, t1, t2;
     h.tag(t0, t1, t2);
     t.word(t0);
@@ -406,37 +554,37 @@ __global__ __launch_bounds__(kPPThreads) void null_open_kernel(
     out_len[i] = res;
 }
 
-// Receiver, grouped: packet p = g * (k + m) + i; a data packet's plaintext goes to its block
-// slot, zero-padded to bb.
+// Receiver, grouped: packet p = g * (k + m) + i, one wave per 64 packets; a data packet's
+// plaintext goes to its block slot, zero-padded to bb, through the wave's LDS tile.
 template <class H>
-__global__ __launch_bounds__(kPPThreads) void open_group_kernel(
+__global__ __launch_bounds__(64) void open_group_kernel(
     int k, int m, int bb, long long n, const uint8_t* __restrict__ pkt, long long pkt_stride,
     const int32_t* __restrict__ pkt_len, const int32_t* __restrict__ ad_len, int ad_all,
     uint8_t* blocks, int32_t* open_len) {
-    const long long p = (long long)blockIdx.x * kPPThreads + threadIdx.x;
-    if (p >= n) return;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const long long p = (long long)blockIdx.x * 64 + threadIdx.x;
     const int per = k + m;
     const long long g = p / per;
     const int i = (int)(p - g * per);
-    const int tl = pkt_len[p], al = len_of(ad_len, ad_all, p);
-    const int cl = tl - al;
-    if (!(tl >= 0 && al >= 0 && cl >= 12 && cl - 12 <= bb && tl <= pkt_stride)) {
-        open_len[p] = -1;
-        return;
+    bool ok = false;
+    int al = 0, cl = 0;
+    if (p < n) {
+        const int tl = pkt_len[p];
+        al = len_of(ad_len, ad_all, p);
+        cl = tl - al;
+        ok = tl >= 0 && al >= 0 && cl >= 12 && cl - 12 <= bb && tl <= pkt_stride;
+        if (!ok) open_len[p] = -1;
     }
-    const uint8_t* pp = pkt + p * pkt_stride;
+    const uint8_t* pp = pkt + (ok ? p : 0) * pkt_stride;
     const uint8_t* c = pp + al;
     H h;
     h.init();
     Sink s;
-    span<true, false>(h, s, pp, al);
-    if (i < k) {
-        s.begin(blocks + (g * k + i) * (long long)bb);
-        span<true, true>(h, s, c + 12, cl - 12);
-        s.zeros_to(s.start + bb);
-    } else {
-        span<true, false>(h, s, c + 12, cl - 12);
-    }
+    if (ok) span<true, false>(h, s, pp, al);
+    const bool data = ok && i < k;
+    tile_stream(h, ok ? c + 12 : nullptr, ok ? cl - 12 : 0,
+                data ? blocks + (g * k + i) * (long long)bb : nullptr, data ? bb : 0, smem);
+    if (!ok) return;
     uint32_t t0, t1, t2;
     h.tag(t0, t1, t2);
     open_len[p] = tag_matches(c, t0, t1, t2) ? cl - 12 : -1;
@@ -541,19 +689,19 @@ unsigned pp_grid(long long n) {
 }
 
 bool pp_grid_ok(long long n) {
-    return (n + kPPThreads - 1) / kPPThreads <= 0x7fffffffLL;
+    return (n + 63) / 64 <= 0x7fffffffLL;
+}
+
+unsigned tile_grid(long long n) {   // one wave (kTilePackets packets) per workgroup
+    return (unsigned)((n + kTilePackets - 1) / kTilePackets);
 }
 
 }  // namespace
 
-// pp_hash: 0 = the six-limb chain (Fnv), 1 = 64-bit halves (Fnv64)
-#define QPP_GO(KERNEL, ...)                                                                 \
-    do {                                                                                   \
-        if (form == 1) qlaunch(KERNEL<Fnv64>, __VA_ARGS__);                                \
-        else qlaunch(KERNEL<Fnv>, __VA_ARGS__);                                            \
-    } while (0)
+// the six-limb FNV chain (a 64-bit-halves form measured within 3 % and was removed, r05)
+#define QPP_GO(KERNEL, ...) qlaunch(KERNEL<Fnv>, __VA_ARGS__)
 
-hipError_t launch_null_seal_h(int form, long long n, const uint8_t* ad, long long ad_stride,
+hipError_t launch_null_seal_h(long long n, const uint8_t* ad, long long ad_stride,
                               const int32_t* ad_len, int ad_all, const uint8_t* pt,
                               long long pt_stride, const int32_t* pt_len, int pt_all,
                               uint8_t* out, long long out_stride, int32_t* out_len,
@@ -562,8 +710,8 @@ hipError_t launch_null_seal_h(int form, long long n, const uint8_t* ad, long lon
     if (!pp_grid_ok(n)) return hipErrorInvalidValue;
     const PtRows pr{nullptr, pt, pt_stride, 0, 1};
     note_kernel("null_seal_kernel");
-    QPP_GO(null_seal_kernel, dim3(pp_grid(n)), dim3(kPPThreads), 0, st, n, ad, ad_stride, ad_len,
-           ad_all, pr, pt_len, pt_all, out, out_stride, out_len);
+    QPP_GO(null_seal_kernel, dim3(tile_grid(n)), dim3(64), kTileBytes, st, n, ad, ad_stride,
+           ad_len, ad_all, pr, pt_len, pt_all, out, out_stride, out_len);
     return hipGetLastError();
 }
 
@@ -571,11 +719,11 @@ hipError_t launch_null_seal(long long n, const uint8_t* ad, long long ad_stride,
                             const int32_t* ad_len, int ad_all, const uint8_t* pt,
                             long long pt_stride, const int32_t* pt_len, int pt_all, uint8_t* out,
                             long long out_stride, int32_t* out_len, hipStream_t st) {
-    return launch_null_seal_h(0, n, ad, ad_stride, ad_len, ad_all, pt, pt_stride, pt_len, pt_all,
+    return launch_null_seal_h(n, ad, ad_stride, ad_len, ad_all, pt, pt_stride, pt_len, pt_all,
                               out, out_stride, out_len, st);
 }
 
-hipError_t launch_null_seal_groups(int form, int k, int m, int bb, long long groups,
+hipError_t launch_null_seal_groups(int k, int m, int bb, long long groups,
                                    const uint8_t* data, const uint8_t* parity, const uint8_t* hdr,
                                    long long hdr_stride, const int32_t* hdr_len, int hdr_all,
                                    const int32_t* pt_len, int pt_all, uint8_t* out,
@@ -585,12 +733,12 @@ hipError_t launch_null_seal_groups(int form, int k, int m, int bb, long long gro
     if (!pp_grid_ok(n)) return hipErrorInvalidValue;
     const PtRows pr{data, parity, bb, k, m};
     note_kernel("null_seal_kernel<groups>");
-    QPP_GO(null_seal_kernel, dim3(pp_grid(n)), dim3(kPPThreads), 0, st, n, hdr, hdr_stride,
+    QPP_GO(null_seal_kernel, dim3(tile_grid(n)), dim3(64), kTileBytes, st, n, hdr, hdr_stride,
            hdr_len, hdr_all, pr, pt_len, pt_all, out, out_stride, out_len);
     return hipGetLastError();
 }
 
-hipError_t launch_null_open_h(int form, long long n, const uint8_t* pkt, long long pkt_stride,
+hipError_t launch_null_open_h(long long n, const uint8_t* pkt, long long pkt_stride,
                               const int32_t* pkt_len, int pkt_all, const int32_t* ad_len,
                               int ad_all, uint8_t* out, long long out_stride, int32_t* out_len,
                               hipStream_t st) {
@@ -606,11 +754,11 @@ hipError_t launch_null_open(long long n, const uint8_t* pkt, long long pkt_strid
                             const int32_t* pkt_len, int pkt_all, const int32_t* ad_len,
                             int ad_all, uint8_t* out, long long out_stride, int32_t* out_len,
                             hipStream_t st) {
-    return launch_null_open_h(0, n, pkt, pkt_stride, pkt_len, pkt_all, ad_len, ad_all, out,
+    return launch_null_open_h(n, pkt, pkt_stride, pkt_len, pkt_all, ad_len, ad_all, out,
                               out_stride, out_len, st);
 }
 
-hipError_t launch_open_groups(int form, int k, int m, int bb, long long groups,
+hipError_t launch_open_groups(int k, int m, int bb, long long groups,
                               const uint8_t* pkt, long long pkt_stride, const int32_t* pkt_len,
                               const int32_t* ad_len, int ad_all, uint8_t* blocks,
                               uint8_t* rows, int32_t* open_len, hipStream_t st) {
@@ -620,7 +768,7 @@ hipError_t launch_open_groups(int form, int k, int m, int bb, long long groups,
     const long long wg = (groups + kAsmWaves - 1) / kAsmWaves;
     if (wg > 0x7fffffffLL) return hipErrorInvalidValue;
     note_kernel("open_group_kernel + open_assemble_kernel");
-    QPP_GO(open_group_kernel, dim3(pp_grid(n)), dim3(kPPThreads), 0, st, k, m, bb, n, pkt,
+    QPP_GO(open_group_kernel, dim3(tile_grid(n)), dim3(64), kTileBytes, st, k, m, bb, n, pkt,
            pkt_stride, pkt_len, ad_len, ad_all, blocks, open_len);
     qlaunch(open_assemble_kernel, dim3((unsigned)wg), dim3(kAsmWaves * 64), 0, st, k, m, bb,
             groups, pkt, pkt_stride, ad_len, ad_all, open_len, blocks, rows);

@@ -467,7 +467,7 @@ OPTION_SETS = [
 # measured-and-rejected variants and timing probes are not options of the product ABI
 # (DESIGN.md section 3.7): qfec_ctx_set_option refuses them with -2
 REMOVED_OPTIONS = ["psyn_ablate", "enc_split", "wide_st", "stream_rc16", "dcol_rows", "dcol_cache",
-                   "psyn_jump", "psyn_pf", "psyn_depth", "ring_nt", "dec_nt", "stream_jump"]
+                   "psyn_jump", "psyn_pf", "psyn_depth", "ring_nt", "dec_nt", "stream_jump", "pp_hash"]
 
 
 @pytest.mark.parametrize("name", REMOVED_OPTIONS)

@@ -22,14 +22,11 @@ def _host(t):
     return t.cpu().numpy()
 
 
-@pytest.fixture(params=[0, 1], ids=["limbs", "halves"])
-def pp_engine(request, engine):
-    """The engine with either FNV-1a-128 chain (context option pp_hash)."""
-    engine.set_option("pp_hash", request.param)
-    try:
-        yield engine
-    finally:
-        engine.set_option("pp_hash", 0)
+@pytest.fixture
+def pp_engine(engine):
+    """The engine (one FNV-1a-128 chain: six 22-bit limbs; the 64-bit-halves form was removed
+    in r05)."""
+    yield engine
 
 
 def test_known_answer_through_gpu(pp_engine):

@@ -29,7 +29,8 @@ def main():
                 name = r["Kernel_Name"]
                 if "qfec" not in name or a.match not in name:
                     continue
-                short = name.split("(")[0].replace("void ", "").replace("qfec::(anonymous namespace)::", "")
+                short = (name.replace("void ", "").replace("(anonymous namespace)::", "")
+                         .split("(")[0])
                 vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
                 key = (short, r["Dispatch_Id"])
                 if key not in seen and r["Dispatch_Id"] in kt:
