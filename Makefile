@@ -82,7 +82,7 @@ $(ROOT)build/gf_stream.o: $(CSRC)/gf_stream.hip $(CSRC)/gf_winjump.h $(HDRS) $(G
 	$(HIPCC) $(HIPFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }
 
-$(ROOT)build/gf_bsyn.o: $(CSRC)/gf_bsyn.hip $(HDRS) $(GEN)
+$(ROOT)build/gf_bsyn.o: $(CSRC)/gf_bsyn.hip $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }

@@ -32,6 +32,7 @@
 #include "fec_kernels.h"
 #include "gf256.h"
 #include "gf_bitslice.h"
+#include "gf_winjump.h"
 
 namespace qfec {
 
@@ -306,9 +307,8 @@ __global__ __launch_bounds__(kBsynWaves * 64) void gf_bsyn_kernel(
                     }
                 });
                 expand_wz(v);
-                const uint32_t cf = (sw >> (8 * ii)) & 0xFFu;
-                apply_nibble<0>(o, cf & 15u, v);
-                apply_nibble<4>(o, cf >> 4, v);
+                // the product by two nibble jumps (gf_winjump.h), not two branch trees
+                wz_mul_acc_rt(o, v, (sw >> (8 * ii)) & 0xFFu);
             }
             const int oslot = slots ? (int)((bsyn_cload_u32(slots, (int)((g * rmax + j) & ~3LL)) >>
                                              (8 * ((g * rmax + j) & 3))) & 0xFFu)
