@@ -634,7 +634,7 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
                 win_build(v.W8, win);
                 static_for<RC>([&](auto jc) __attribute__((always_inline)) {
                     constexpr int j = decltype(jc)::value;
-                    win_apply<cauchy_coef_small(MC, j, x)>(acc[j], win);
+                    win_apply<cauchy_coef(MC, j, x)>(acc[j], win);
                 });
             } else {
                 uint32_t cwv[NCW];
@@ -842,9 +842,12 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     }
     // the static ring schedule is used for the encode only: its rolled decode measured
     // slower than gf_stream's (0.644 vs 0.619 ms on config B)
-    if (t.stream_static && !decode && k == 32 && s == 169 && m == 4 && t.const_enc &&
+    const bool ring_shape = (k == 32 && m == 4) || (k == 10 && (m == 10 || m == 15 || m == 20)) ||
+                            (k == 250 && m == 5);
+    if (t.stream_static && !decode && s == 169 && ring_shape && t.const_enc &&
         ((long long)k * bb) % 16 == 0) {
-        // the fixed B/C shape: compile-time ring schedule (gf_ring_kernel)
+        // the fixed B/C shape and the even-k QuicR presets: compile-time ring schedule
+        // (gf_ring_kernel)
         const size_t rlds = (size_t)kRingWaves * RingShape<169>::RB;
         const long long rwant = (groups + kRingWaves - 1) / kRingWaves;
         long long rcap = (long long)t.cus * (int)((160 * 1024) / rlds);
@@ -853,12 +856,18 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         if ((groups + (long long)rgrid * kRingWaves - 1) / ((long long)rgrid * kRingWaves) >=
             (1LL << 31))
             return hipErrorInvalidValue;
-#define QR_GO(RCV, DEC, MCV, NTV)                                                              \
-    qlaunch((gf_ring_kernel<32, 169, RCV, DEC, MCV, NTV>), dim3(rgrid),              \
+#define QR_GO(KV, MCV)                                                                          \
+    qlaunch((gf_ring_kernel<KV, 169, MCV, false, MCV, true>), dim3(rgrid),                       \
                        dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax, \
                        coef_gstride, out_gstride)
-        note_kernel("gf_ring_kernel<encode,k32m4>");
-        QR_GO(4, false, 4, true);   // nt parity stores (plain: 0.673 vs 0.578 ms)
+        // nt parity stores (plain: 0.673 vs 0.578 ms on B)
+        switch (k * 256 + m) {
+            case 32 * 256 + 4: note_kernel("gf_ring_kernel<encode,k32m4>"); QR_GO(32, 4); break;
+            case 10 * 256 + 10: note_kernel("gf_ring_kernel<encode,k10m10>"); QR_GO(10, 10); break;
+            case 10 * 256 + 15: note_kernel("gf_ring_kernel<encode,k10m15>"); QR_GO(10, 15); break;
+            case 250 * 256 + 5: note_kernel("gf_ring_kernel<encode,k250m5>"); QR_GO(250, 5); break;
+            default: note_kernel("gf_ring_kernel<encode,k10m20>"); QR_GO(10, 20); break;
+        }
 #undef QR_GO
         return hipGetLastError();
     }

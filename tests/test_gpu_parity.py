@@ -743,16 +743,19 @@ PRESETS = [(5, 5), (10, 10), (10, 15), (10, 20), (15, 15), (250, 5)]   # quic_fe
 
 
 PSYN = {(10, 10), (10, 15), (10, 20), (15, 15)}   # m >= 7: gf_psyn's compiled syndrome decode
+RING_ENC = {(10, 10), (10, 15), (10, 20), (250, 5)}   # even k: gf_ring's static schedule
 
 
 @pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0},
-                                  {"psyn": 0, "stream_grid": 1}],
-                         ids=["default", "grid1", "runtime", "runtime_grid1"])
+                                  {"psyn": 0, "stream_grid": 1}, {"stream_static": 0}],
+                         ids=["default", "grid1", "runtime", "runtime_grid1", "no_ring"])
 @pytest.mark.parametrize("k,m", PRESETS)
 def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
     """QuicR's negotiated configurations with 1350-byte payloads (bb = 1352): odd k puts every
     other group 8 bytes off a 16-byte boundary, m > 8 and more than 8 losses cut the run-time
-    decode's outputs into chunks.  Encodes run the compiled gf_stream; decodes run gf_psyn
+    decode's outputs into chunks.  Encodes run gf_ring's static schedule for the even-k
+    presets (gf_stream with stream_static = 0) and the compiled gf_stream for the others;
+    decodes run gf_psyn
     (compiled syndromes + Gauss-Jordan) for the m >= 7 presets and gf_stream for the others,
     never gf_apply; with psyn = 0, the run-time gf_stream decode (nibble-jump products) for
     every preset.  The (5, 5) encode writes its parity through LDS-staged wide stores.  Bit-exact vs the oracle in every decode layout, with as many losses as
@@ -765,7 +768,9 @@ def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
     data = synth.group_data(9000 + k + m, k, bb, G)
     p_or, rc_or = oracle.encode_batch(k, m, bb, data)
     p_gpu, rc = gpu_encode(engine, k, m, bb, data)
-    assert fec.last_kernels().startswith("gf_stream_kernel<encode"), fec.last_kernels()
+    enc = ("gf_ring_kernel<encode" if (k, m) in RING_ENC and opts.get("stream_static", 1)
+           else "gf_stream_kernel<encode")
+    assert fec.last_kernels().startswith(enc), fec.last_kernels()
     assert rc == rc_or == 0
     np.testing.assert_array_equal(p_gpu, p_or)
     dec = ("gf_psyn_kernel<decode" if (k, m) in PSYN and opts.get("psyn", 1)

@@ -11,6 +11,7 @@
 #   preset:<k>,<m>        quick bench of a QuicR preset
 #   prof:<W>[:<args>]     rocprofv3 --kernel-trace --stats of a quick bench
 #   abold:<W>[:<args>]    quick bench against quic_amd/libquic_fec_abold.so (an A/B build)
+#   aboldp:<k>,<m>        the same for a QuicR preset
 #   pmc:<W>[:<args>]      tools/pmc.sh passes (FETCH/WRITE traffic, waves, issue mix)
 # Extra args use '+' for spaces: quick:B:--opt+ring_nt=0.  GPU_STEPS_DRY=1 prints the steps.
 export TMPDIR=/tmp
@@ -35,6 +36,7 @@ for step in "$@"; do
     bench)  specs+=("$tag::600::python bench.py --workload $W --verify $extra") ;;
     quick)  specs+=("$tag::300::$quick --workload $W $extra") ;;
     preset) specs+=("$tag::300::$quick --preset $W $extra") ;;
+    aboldp) specs+=("$tag::300::QFEC_LIB_PATH=quic_amd/libquic_fec_abold.so $quick --preset $W $extra") ;;
     abold)  specs+=("$tag::300::QFEC_LIB_PATH=quic_amd/libquic_fec_abold.so $quick --workload $W $extra") ;;
     prof)   specs+=("$tag::300::rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run --output-format csv -- $quick --workload $W $extra") ;;
     pmc)    specs+=("$tag::600::bash tools/pmc.sh $W $tag $extra") ;;
