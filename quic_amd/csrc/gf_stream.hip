@@ -458,14 +458,16 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gf_stream_kernel(
 // wrapped addresses.
 constexpr int kRingWaves = 4;
 
-template <int S>
+// SK: the group's bytes start SK bytes into its stream (odd k at 1352-byte blocks: groups
+// alternate between 0 and 8 bytes past a 16-byte boundary)
+template <int S, int SK = 0>
 struct RingShape {
     static constexpr int R = 8, RB = R * 1024;
     static constexpr int BB = 8 * S;
     static constexpr int NW = (S + 3) / 4, NWF = S / 4;
     static constexpr int SPR = 1 + ((S >> 1) & 1) + (S & 1);
-    static constexpr int pf(int x) { return (x * BB) >> 10; }             // first piece of block x
-    static constexpr int pl(int x) { return ((x + 1) * BB - 1) >> 10; }   // its last piece
+    static constexpr int pf(int x) { return (SK + x * BB) >> 10; }             // first piece of block x
+    static constexpr int pl(int x) { return (SK + (x + 1) * BB - 1) >> 10; }   // its last piece
     // smallest count of VMEM instructions younger than a block's last piece when the wave
     // waits for it (K blocks per group, NST stores per group): one conservative immediate
     // for the rolled (run-time block index) form
@@ -481,15 +483,22 @@ struct RingShape {
     }
 };
 
-// NT: the encode's parity stores are non-temporal (ring_nt option; decode stores plain)
-template <int K, int S, int RC, bool DECODE, int MC, bool NT = true>
-__global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
+// NT: the encode's parity stores are non-temporal (decode stores plain).  SK: see RingShape.
+// A group whose size is 8 mod 16 is streamed as GBS = GB + 8 bytes from the 16-byte boundary
+// at or below its start; the loads then go through a buffer resource bounded by the end of
+// the input (the last group's stream may end 8 bytes past it: those lanes read zeros).
+template <int K, int S, int RC, bool DECODE, int MC, bool NT, int SK>
+__device__ __forceinline__ void gf_ring_run(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
-    int rmax, long long coef_gstride, long long out_gstride) {
-    using SH = RingShape<S>;
+    int rmax, long long coef_gstride, long long out_gstride, uint8_t* smem) {
+    using SH = RingShape<S, SK>;
     constexpr int R = SH::R, RB = SH::RB, BB = SH::BB, NW = SH::NW, NWF = SH::NWF;
-    constexpr int GB = K * BB, NP = (GB + 1023) / 1024;
+    constexpr int GB = K * BB;
+    constexpr bool SKEW = GB % 16 != 0;
+    constexpr int GBS = (GB + 15) / 16 * 16;              // stream bytes per group
+    constexpr int NP = (GBS + 1023) / 1024;
+    static_assert(SKEW ? GB % 16 == 8 : SK == 0, "groups 0 or 8 bytes off 16");
     constexpr int NST = RC * 8 * SH::SPR;                 // stores per group, fixed
     constexpr int RCP = RC < 4 ? 4 : RC, NCW = RCP / 4;
     constexpr int SAUX = (DECODE || !NT) ? 0 : 2;         // encode's parity stream: nt
@@ -498,7 +507,6 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
     static_assert(DECODE || MC == RC, "encode: one output per register set");
     static_assert(FM1 >= SH::pl(0), "block 0 of the next group is prefetched in full");
     static_assert(NP > R, "a group spans more than the ring");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63;
     const int w = wave_id();
     uint8_t* ring = smem + (size_t)w * RB;
@@ -510,27 +518,40 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
     const int c = lane < NW ? lane : NW - 1;              // idle lanes shadow the last word
     const long long gstep = W * GB;
 
-    const uint8_t* gsrc = in + g0 * GB;                   // current group's bytes
+    const uint8_t* gsrc = in + g0 * GB - SK;              // current group's stream
+    const uint8_t* in_end = in + groups * GB;
     int phase = 0;                                        // ring slot of its piece 0
     long long i = 0;                                      // current group
+
+    // piece p of the stream that starts at src into ring slot `slot`.  The skewed form puts
+    // the piece's offset into the descriptor's base (the range check then bounds the piece,
+    // and the lane offsets are two loop-invariant VGPRs instead of one per piece)
+    const uint32_t v16 = 16u * (uint32_t)lane;
+    const uint32_t vlast = min(16u * (uint32_t)lane, (uint32_t)(GBS - 16 - (NP - 1) * 1024));
+    auto dma = [&](const uint8_t* src, int p, int slot) __attribute__((always_inline)) {
+        if constexpr (SKEW) {
+            const uint8_t* b = src + p * 1024;
+            const long long left = in_end - b;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)b, 0, (unsigned)(left < 1024 ? left : 1024), 0x00020000);
+            stream_dma16(rs, ring + slot * 1024, p == NP - 1 ? vlast : v16);
+        } else {
+            const int off = min(p * 1024 + lane * 16, GBS - 16);
+            __builtin_amdgcn_global_load_lds(QS_GPTR(src + off), QS_LPTR(ring + slot * 1024), 16,
+                                             0, 2);
+        }
+    };
 
     // piece n of the current group (n >= NP: piece n - NP of the next, or a dummy reread
     // of the current group's last piece when there is no next group)
     auto issue = [&](auto nc) __attribute__((always_inline)) {
         constexpr int n = decltype(nc)::value;
-        const uint8_t* src;
-        int off;
         if constexpr (n < NP) {
-            src = gsrc;
-            off = min(n * 1024 + lane * 16, GB - 16);
+            dma(gsrc, n, (phase + n) & (R - 1));
         } else {
             const bool next = i + 1 < cnt;
-            src = next ? gsrc + gstep : gsrc;
-            off = min((next ? n - NP : NP - 1) * 1024 + lane * 16, GB - 16);
+            dma(next ? gsrc + gstep : gsrc, next ? n - NP : NP - 1, (phase + n) & (R - 1));
         }
-        const int slot = (phase + n) & (R - 1);
-        __builtin_amdgcn_global_load_lds(QS_GPTR(src + off), QS_LPTR(ring + slot * 1024), 16, 0,
-                                         2);
     };
     // the same for a run-time piece index (rolled decode loop)
     auto issue_rt = [&](int n) __attribute__((always_inline)) {
@@ -541,10 +562,7 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
             src = next ? gsrc + gstep : gsrc;
             p = next ? n - NP : NP - 1;
         }
-        const int off = min(p * 1024 + lane * 16, GB - 16);
-        const int slot = (phase + n) & (R - 1);
-        __builtin_amdgcn_global_load_lds(QS_GPTR(src + off), QS_LPTR(ring + slot * 1024), 16, 0,
-                                         2);
+        dma(src, p, (phase + n) & (R - 1));
     };
     // block x (an int or an integral_constant) at ring byte (phase * 1024 + x * BB) mod RB
     auto read_block = [&](auto xc, uint32_t (&lo)[8], uint32_t (&hi)[8])
@@ -552,7 +570,7 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
         const int x = xc;
         uint32_t c4 = 4u * (uint32_t)c;
         asm volatile("" : "+v"(c4));   // opaque: addresses are not hoisted across blocks
-        uint32_t bp = ((uint32_t)phase * 1024u + (uint32_t)(x * BB)) & (uint32_t)(RB - 1);
+        uint32_t bp = ((uint32_t)phase * 1024u + (uint32_t)(SK + x * BB)) & (uint32_t)(RB - 1);
         if (bp + (uint32_t)BB + 4u <= (uint32_t)RB) {
             const uint8_t* L = ring + bp + c4;
 #pragma unroll
@@ -737,6 +755,28 @@ __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
     stream_wait_vmcnt<0>();
 }
 
+template <int K, int S, int RC, bool DECODE, int MC, bool NT = true>
+__global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
+    const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
+    const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
+    int rmax, long long coef_gstride, long long out_gstride) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if constexpr ((K * 8 * S) % 16 == 0) {
+        gf_ring_run<K, S, RC, DECODE, MC, NT, 0>(in, out, coef, slots, nout, groups, rmax,
+                                                  coef_gstride, out_gstride, smem);
+    } else {
+        // group g starts 8 * (g & 1) bytes past a 16-byte boundary; a wave's groups g0,
+        // g0 + W, ... (W = 4 x the grid, even) all share g0's skew
+        const long long g0 = (long long)blockIdx.x * kRingWaves + wave_id();
+        if (g0 & 1)
+            gf_ring_run<K, S, RC, DECODE, MC, NT, 8>(in, out, coef, slots, nout, groups, rmax,
+                                                      coef_gstride, out_gstride, smem);
+        else
+            gf_ring_run<K, S, RC, DECODE, MC, NT, 0>(in, out, coef, slots, nout, groups, rmax,
+                                                      coef_gstride, out_gstride, smem);
+    }
+}
+
 // Ring slots the stream needs: before block x's compute the ring keeps every piece from
 // block x's first on, and block x + 1 must land in it too.  Blocks x and x + 1 span
 // (o + 2 * bb + 1023) / 1024 pieces from block x's head piece, o its start offset in that
@@ -843,9 +883,8 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     // the static ring schedule is used for the encode only: its rolled decode measured
     // slower than gf_stream's (0.644 vs 0.619 ms on config B)
     const bool ring_shape = (k == 32 && m == 4) || (k == 10 && (m == 10 || m == 15 || m == 20)) ||
-                            (k == 250 && m == 5);
-    if (t.stream_static && !decode && s == 169 && ring_shape && t.const_enc &&
-        ((long long)k * bb) % 16 == 0) {
+                            (k == 250 && m == 5) || (k == 15 && m == 15);
+    if (t.stream_static && !decode && s == 169 && ring_shape && t.const_enc) {
         // the fixed B/C shape and the even-k QuicR presets: compile-time ring schedule
         // (gf_ring_kernel)
         const size_t rlds = (size_t)kRingWaves * RingShape<169>::RB;
@@ -866,6 +905,7 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
             case 10 * 256 + 10: note_kernel("gf_ring_kernel<encode,k10m10>"); QR_GO(10, 10); break;
             case 10 * 256 + 15: note_kernel("gf_ring_kernel<encode,k10m15>"); QR_GO(10, 15); break;
             case 250 * 256 + 5: note_kernel("gf_ring_kernel<encode,k250m5>"); QR_GO(250, 5); break;
+            case 15 * 256 + 15: note_kernel("gf_ring_kernel<encode,k15m15>"); QR_GO(15, 15); break;
             default: note_kernel("gf_ring_kernel<encode,k10m20>"); QR_GO(10, 20); break;
         }
 #undef QR_GO
