@@ -24,7 +24,8 @@ struct Tune {
     int stream = 1;           // m > 1, small blocks: gf_stream (0: gf_apply)
     int stream_ring = 8;      // gf_stream: 1 KiB ring slots per wave (4..36), + 2 mirrored
     int stream_grid = 0;      // gf_stream: grid cap in workgroups (0: CUs x per-CU fit)
-    int stream_static = 1;    // gf_stream: compile-time ring schedule for k = 32, bb = 1352
+    int stream_static = 1;    // gf_ring: compile-time ring schedule (B/C and preset encodes)
+    int ring_wide = 1;        // gf_ring preset encodes: LDS-staged 8-byte parity stores
     int const_enc = 1;        // encode kernels specialised for fixed (k, m) where compiled
     int pd = 2;               // gf_apply: register pipeline depth (1..3)
     int flat = 1;             // gf_apply: lane-flat encode

@@ -487,7 +487,7 @@ struct RingShape {
 // A group whose size is 8 mod 16 is streamed as GBS = GB + 8 bytes from the 16-byte boundary
 // at or below its start; the loads then go through a buffer resource bounded by the end of
 // the input (the last group's stream may end 8 bytes past it: those lanes read zeros).
-template <int K, int S, int RC, bool DECODE, int MC, bool NT, int SK>
+template <int K, int S, int RC, bool DECODE, int MC, bool NT, int SK, bool WIDE>
 __device__ __forceinline__ void gf_ring_run(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
@@ -499,7 +499,9 @@ __device__ __forceinline__ void gf_ring_run(
     constexpr int GBS = (GB + 15) / 16 * 16;              // stream bytes per group
     constexpr int NP = (GBS + 1023) / 1024;
     static_assert(SKEW ? GB % 16 == 8 : SK == 0, "groups 0 or 8 bytes off 16");
-    constexpr int NST = RC * 8 * SH::SPR;                 // stores per group, fixed
+    // stores per group, fixed: 8 sub-rows x SPR per output, or (WIDE) 3 runs of 512 bytes
+    constexpr int NST = WIDE ? RC * 3 : RC * 8 * SH::SPR;
+    static_assert(!WIDE || (S == 169 && !DECODE), "wide stores: 1352-byte encode blocks");
     constexpr int RCP = RC < 4 ? 4 : RC, NCW = RCP / 4;
     constexpr int SAUX = (DECODE || !NT) ? 0 : 2;         // encode's parity stream: nt
     constexpr int FM1 = SH::pf(K - 1) + R - 1 - NP;       // next-group pieces issued early
@@ -510,6 +512,9 @@ __device__ __forceinline__ void gf_ring_run(
     const int lane = threadIdx.x & 63;
     const int w = wave_id();
     uint8_t* ring = smem + (size_t)w * RB;
+    const uint32_t stage =   // (WIDE) this wave's staging buffer (LDS address), after the rings
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(
+            smem + (size_t)kRingWaves * RB + (size_t)w * kStreamStage);
     const long long W = (long long)gridDim.x * kRingWaves;
     const long long g0 = (long long)blockIdx.x * kRingWaves + w;
     if (g0 >= groups) return;
@@ -727,6 +732,36 @@ __device__ __forceinline__ void gf_ring_run(
         // ---- outputs: NST store instructions whatever n is (unused outputs: empty range),
         // kept after the last step's DMAs and before the next group's (issue order)
         asm volatile("" ::: "memory");
+        if constexpr (WIDE) {
+            // each parity block staged in LDS as its contiguous bytes (stage_block_169), read
+            // back as 3 x 512 bytes and stored as 8-byte lanes (past the block: dropped by the
+            // buffer range)
+            const uint32_t ra = stage + 8u * (uint32_t)lane;
+#pragma unroll
+            for (int j = 0; j < RC; ++j) {
+                uint8_t* dst = out + g * out_gstride + (long long)j * BB;
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc(dst, 0, (unsigned)BB, 0x00020000);
+                if (lane < NW) stage_block_169(stage, acc[j], lane);
+                uint64_t v0, v1, v2;
+                asm volatile("ds_read_b64 %0, %3\n\t"
+                             "ds_read_b64 %1, %3 offset:512\n\t"
+                             "ds_read_b64 %2, %3 offset:1024\n\t"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=&v"(v0), "=&v"(v1), "=&v"(v2)
+                             : "v"(ra)
+                             : "memory");
+                const uint64_t vv[3] = {v0, v1, v2};
+#pragma unroll
+                for (int h = 0; h < 3; ++h)
+                    __builtin_amdgcn_raw_buffer_store_b64(qf_u32x2(vv[h]), rs,
+                                                          512u * h + 8u * (uint32_t)lane, 0, SAUX);
+            }
+            asm volatile("" ::: "memory");
+            gsrc += gstep;
+            phase = (phase + NP) & (R - 1);
+            continue;
+        }
         uint32_t vo = lane < NWF ? 4u * (uint32_t)c : kSDrop;
         uint32_t vt = lane == NWF && NWF < NW ? 4u * (uint32_t)c : kSDrop;
         asm volatile("" : "+v"(vo), "+v"(vt));
@@ -755,24 +790,24 @@ __device__ __forceinline__ void gf_ring_run(
     stream_wait_vmcnt<0>();
 }
 
-template <int K, int S, int RC, bool DECODE, int MC, bool NT = true>
+template <int K, int S, int RC, bool DECODE, int MC, bool NT = true, bool WIDE = false>
 __global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
     int rmax, long long coef_gstride, long long out_gstride) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if constexpr ((K * 8 * S) % 16 == 0) {
-        gf_ring_run<K, S, RC, DECODE, MC, NT, 0>(in, out, coef, slots, nout, groups, rmax,
+        gf_ring_run<K, S, RC, DECODE, MC, NT, 0, WIDE>(in, out, coef, slots, nout, groups, rmax,
                                                   coef_gstride, out_gstride, smem);
     } else {
         // group g starts 8 * (g & 1) bytes past a 16-byte boundary; a wave's groups g0,
         // g0 + W, ... (W = 4 x the grid, even) all share g0's skew
         const long long g0 = (long long)blockIdx.x * kRingWaves + wave_id();
         if (g0 & 1)
-            gf_ring_run<K, S, RC, DECODE, MC, NT, 8>(in, out, coef, slots, nout, groups, rmax,
+            gf_ring_run<K, S, RC, DECODE, MC, NT, 8, WIDE>(in, out, coef, slots, nout, groups, rmax,
                                                       coef_gstride, out_gstride, smem);
         else
-            gf_ring_run<K, S, RC, DECODE, MC, NT, 0>(in, out, coef, slots, nout, groups, rmax,
+            gf_ring_run<K, S, RC, DECODE, MC, NT, 0, WIDE>(in, out, coef, slots, nout, groups, rmax,
                                                       coef_gstride, out_gstride, smem);
     }
 }
@@ -887,7 +922,13 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     if (t.stream_static && !decode && s == 169 && ring_shape && t.const_enc) {
         // the fixed B/C shape and the even-k QuicR presets: compile-time ring schedule
         // (gf_ring_kernel)
-        const size_t rlds = (size_t)kRingWaves * RingShape<169>::RB;
+        // wide (LDS-staged 8-byte) parity stores: 3 store instructions per block instead of
+        // 16, so the group's store count stays under the 63 a counted wait can name.  Not for
+        // (10, 20): 290 VGPRs, one wave per SIMD (0.754 vs 0.673 ms); B/C keep 4 x 16 stores
+        // 
+        const bool rwide = t.ring_wide && !(k == 32 && m == 4) && !(k == 10 && m == 20) &&
+                           (((uintptr_t)out | (uintptr_t)out_gstride) & 7) == 0;
+        const size_t rlds = (size_t)kRingWaves * (RingShape<169>::RB + (rwide ? kStreamStage : 0));
         const long long rwant = (groups + kRingWaves - 1) / kRingWaves;
         long long rcap = (long long)t.cus * (int)((160 * 1024) / rlds);
         if (t.stream_grid > 0) rcap = t.stream_grid;
@@ -895,20 +936,26 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         if ((groups + (long long)rgrid * kRingWaves - 1) / ((long long)rgrid * kRingWaves) >=
             (1LL << 31))
             return hipErrorInvalidValue;
-#define QR_GO(KV, MCV)                                                                          \
-    qlaunch((gf_ring_kernel<KV, 169, MCV, false, MCV, true>), dim3(rgrid),                       \
+#define QR_GO1(KV, MCV, WV)                                                                     \
+    qlaunch((gf_ring_kernel<KV, 169, MCV, false, MCV, true, WV>), dim3(rgrid),                   \
                        dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax, \
                        coef_gstride, out_gstride)
+#define QR_GO(KV, MCV)                  \
+    do {                                \
+        if (rwide) QR_GO1(KV, MCV, true); \
+        else QR_GO1(KV, MCV, false);      \
+    } while (0)
         // nt parity stores (plain: 0.673 vs 0.578 ms on B)
         switch (k * 256 + m) {
-            case 32 * 256 + 4: note_kernel("gf_ring_kernel<encode,k32m4>"); QR_GO(32, 4); break;
+            case 32 * 256 + 4: note_kernel("gf_ring_kernel<encode,k32m4>"); QR_GO1(32, 4, false); break;
             case 10 * 256 + 10: note_kernel("gf_ring_kernel<encode,k10m10>"); QR_GO(10, 10); break;
             case 10 * 256 + 15: note_kernel("gf_ring_kernel<encode,k10m15>"); QR_GO(10, 15); break;
             case 250 * 256 + 5: note_kernel("gf_ring_kernel<encode,k250m5>"); QR_GO(250, 5); break;
             case 15 * 256 + 15: note_kernel("gf_ring_kernel<encode,k15m15>"); QR_GO(15, 15); break;
-            default: note_kernel("gf_ring_kernel<encode,k10m20>"); QR_GO(10, 20); break;
+            default: note_kernel("gf_ring_kernel<encode,k10m20>"); QR_GO1(10, 20, false); break;
         }
 #undef QR_GO
+#undef QR_GO1
         return hipGetLastError();
     }
     if (decode) {

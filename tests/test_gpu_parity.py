@@ -747,8 +747,10 @@ RING_ENC = {(10, 10), (10, 15), (10, 20), (15, 15), (250, 5)}   # gf_ring's stat
 
 
 @pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0},
-                                  {"psyn": 0, "stream_grid": 1}, {"stream_static": 0}],
-                         ids=["default", "grid1", "runtime", "runtime_grid1", "no_ring"])
+                                  {"psyn": 0, "stream_grid": 1}, {"stream_static": 0},
+                                  {"ring_wide": 0}, {"ring_wide": 0, "stream_grid": 1}],
+                         ids=["default", "grid1", "runtime", "runtime_grid1", "no_ring",
+                              "ring_plain", "ring_plain_grid1"])
 @pytest.mark.parametrize("k,m", PRESETS)
 def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
     """QuicR's negotiated configurations with 1350-byte payloads (bb = 1352): odd k puts every
