@@ -846,6 +846,7 @@ bool gf_stream_supported(int k, int m, int bb, int rc, bool decode, const Tune& 
     return true;
 }
 
+#ifndef QF_KERNELS_ONLY   // (register-use experiments compile single instantiations)
 hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef,
                             const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
                             long long groups, int rc, int rmax, long long coef_gstride,
@@ -1017,4 +1018,5 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     return hipGetLastError();
 }
 
+#endif
 }  // namespace qfec
