@@ -75,7 +75,12 @@ constexpr int kPsynWaves = 4;   // waves per workgroup (independent)
 // the lanes' DMA offsets (one VALU); and every group issues at least NSTMIN stores (empty-range
 // ones pad a group with fewer than 4 recovered blocks), so the wait for a block DMA'd before
 // the previous group's stores is always vmcnt(63): no wait ladder over the store count.
-template <int KC, int MC, int RC, int S, int D>
+// WIDE: each recovered block is staged in LDS as its contiguous bytes and written as three
+// 512-byte runs of 8-byte lanes (3 store instructions instead of 8 x SPR); every group then
+// issues exactly 3 x RC stores (empty-range ones pad it), so all its waits are exact
+// immediates below 63 instead of the vmcnt(63) that over-waits behind > 63 stores.
+constexpr int kPsynStage = 1360;   // per-wave staging buffer (WIDE), after the rings
+template <int KC, int MC, int RC, int S, int D, bool WIDE = false>
 __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
     const uint8_t* __restrict__ cenc, const uint8_t* __restrict__ slots,
@@ -87,7 +92,10 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
     constexpr int WAITN = D * NPC;            // younger than block b when it is awaited
     constexpr int NSB = 8 * SPR;              // store instructions per recovered block
     constexpr int NSTMIN = 63 - WAITN;        // stores a group issues at least
+    constexpr int NSTW = 3 * RC;              // (WIDE) stores a group issues, exactly
+    constexpr int WAIT0 = WIDE ? WAITN + NSTW : 63;   // a block DMA'd before the last stores
     static_assert(WAITN <= 63 && D >= 2 && KC >= D, "pipeline depth");
+    static_assert(!WIDE || (S == 169 && WAIT0 <= 63), "wide stores: 1352-byte blocks");
     static_assert(KC <= 64 && MC <= 32 && RC <= 16 && RC <= KC && RC <= MC && BB % 8 == 0 &&
                       NB <= 32 && BUFB <= 2048,
                   "compiled small-block code");
@@ -95,6 +103,9 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
 
     const int w = wave_id();
     uint8_t* ring = smem + (size_t)w * NB * BUFB;
+    const uint32_t stage =   // (WIDE) this wave's staging buffer (LDS address)
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(
+            smem + (size_t)kPsynWaves * NB * BUFB + (size_t)w * kPsynStage);
     const long long W = (long long)gridDim.x * kPsynWaves;
     const long long g0 = (long long)blockIdx.x * kPsynWaves + w;
     if (g0 >= groups) return;
@@ -150,7 +161,8 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
         // blocks 0 .. D - 1 are awaited like every other group's
         const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0u, 0x00020000);
 #pragma unroll
-        for (int q = 0; q < NSTMIN; ++q) __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0u, 4 * q, 0);
+        for (int q = 0; q < (WIDE ? NSTW : NSTMIN); ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0u, 4 * q, 0);
     }
     asm volatile("" ::: "memory");
 
@@ -173,7 +185,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
         // were DMA'd before the previous group's >= NSTMIN stores), read and realign it
         auto take = [&](uint32_t (&wv)[8]) __attribute__((always_inline)) {
             issue_next();
-            if (p < D) psyn_wait_vmcnt<63>();
+            if (p < D) psyn_wait_vmcnt<WAIT0>();
             else psyn_wait_vmcnt<WAITN>();
             const int buf = (int)((unsigned)b % NB);
             uint32_t a = 4u * (uint32_t)min((int)__lane_id(), NW - 1) + (uint32_t)(buf * BUFB) +
@@ -299,6 +311,41 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
         // instructions each, non-temporal; a group with fewer than 4 recovered blocks pads to
         // NSTMIN stores with empty-range ones
         asm volatile("" ::: "memory");   // stores stay in issue order among the DMAs
+        if constexpr (WIDE) {
+            const int ln = (int)__lane_id();
+            const uint32_t ra = stage + 8u * (uint32_t)ln;
+            static_for<RC>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int j = decltype(jc)::value;
+                if (j < n) {
+                    const int oslot = slots ? (int)((psyn_cload_u32(slots, (int)((g * rmax + j) & ~3LL)) >>
+                                                     (8 * ((g * rmax + j) & 3))) & 0xFFu)
+                                            : j;
+                    uint8_t* dst = out + g * out_gstride + (long long)oslot * BB;
+                    const __amdgpu_buffer_rsrc_t rs =
+                        __builtin_amdgcn_make_buffer_rsrc(dst, 0, (unsigned)BB, 0x00020000);
+                    if (ln < NW) stage_block_169(stage, acc[j], ln);
+                    uint64_t v0, v1, v2;
+                    asm volatile("ds_read_b64 %0, %3\n\t"
+                                 "ds_read_b64 %1, %3 offset:512\n\t"
+                                 "ds_read_b64 %2, %3 offset:1024\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=&v"(v0), "=&v"(v1), "=&v"(v2)
+                                 : "v"(ra)
+                                 : "memory");
+                    const uint64_t vv[3] = {v0, v1, v2};
+#pragma unroll
+                    for (int h = 0; h < 3; ++h)
+                        __builtin_amdgcn_raw_buffer_store_b64(qf_u32x2(vv[h]), rs,
+                                                              512u * h + 8u * (uint32_t)ln, 0, 2);
+                }
+            });
+            // pad to exactly NSTW stores (empty range)
+            const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0u, 0x00020000);
+#pragma unroll 1
+            for (int q = 3 * n; q < NSTW; ++q) __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0u, 0, 0);
+            asm volatile("" ::: "memory");
+            continue;
+        }
         static_for<RC>([&](auto jc) __attribute__((always_inline)) {
             constexpr int j = decltype(jc)::value;
             if (j < n) {
@@ -342,7 +389,7 @@ constexpr int kPsynS = 169;   // bb = 1352: 1350-byte payloads
 struct PsynLaunch {
     const uint8_t *in; uint8_t *out; const uint8_t *tab, *cenc, *slots; const int32_t *nout;
     long long groups; int rmax; long long out_gstride; hipStream_t st; const Tune *t;
-    int k; size_t lds;
+    int k; size_t lds; bool wide;
 };
 hipError_t psyn_go_1010(const PsynLaunch& a);
 hipError_t psyn_go_1015(const PsynLaunch& a);
@@ -357,7 +404,8 @@ hipError_t psyn_go_1515(const PsynLaunch& a);
     hipError_t NAME(const PsynLaunch& a) {                                                     \
         const Tune& t = *a.t;                                                                  \
         constexpr int RCV = KV < MV ? KV : MV;                                                 \
-        const auto kern = gf_psyn_kernel<KV, MV, RCV, kPsynS, 5>;                    \
+        const auto kern = a.wide ? gf_psyn_kernel<KV, MV, RCV, kPsynS, 5, true>               \
+                                 : gf_psyn_kernel<KV, MV, RCV, kPsynS, 5, false>;             \
         const long long want = (a.groups + kPsynWaves - 1) / kPsynWaves;                       \
         long long cap = (long long)t.cus * resident_blocks((const void*)kern, kPsynWaves * 64, a.lds); \
         if (t.stream_grid > 0) cap = t.stream_grid; /* tests: many groups per wave */          \

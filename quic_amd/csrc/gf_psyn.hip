@@ -306,7 +306,12 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
     PsynLaunch a;
     a.in = in, a.out = out, a.tab = tab, a.cenc = cenc, a.slots = slots, a.nout = nout;
     a.groups = groups, a.rmax = rmax, a.out_gstride = out_gstride, a.st = st, a.t = &t, a.k = k;
-    a.lds = (size_t)kPsynWaves * (5 + 1) * SH::BUFB;   // ring depth 5
+    // wide recovered-block stores: measured faster for (10, 10) only (0.370-0.382 -> 0.348-
+    // 0.356 ms; (15, 15) and (10, 20) unchanged, (10, 15) 0.392 -> 0.410), so psyn_wide = 1
+    // (default) takes them there and psyn_wide = 2 for every code; out 8-byte aligned
+    a.wide = (t.psyn_wide == 2 || (t.psyn_wide == 1 && k == 10 && m == 10)) &&
+             ((((uintptr_t)out) | (uintptr_t)out_gstride) & 7) == 0;
+    a.lds = (size_t)kPsynWaves * ((5 + 1) * SH::BUFB + (a.wide ? kPsynStage : 0));   // ring depth 5
     note_kernel("gf_psyn_kernel<decode,preset>");
     switch (k * 256 + m) {
         case 10 * 256 + 10: return psyn_go_1010(a);

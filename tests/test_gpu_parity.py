@@ -748,9 +748,10 @@ RING_ENC = {(10, 10), (10, 15), (10, 20), (15, 15), (250, 5)}   # gf_ring's stat
 
 @pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0},
                                   {"psyn": 0, "stream_grid": 1}, {"stream_static": 0},
-                                  {"ring_wide": 0}, {"ring_wide": 0, "stream_grid": 1}],
+                                  {"ring_wide": 0}, {"ring_wide": 0, "stream_grid": 1},
+                                  {"psyn_wide": 2}, {"psyn_wide": 0, "stream_grid": 1}],
                          ids=["default", "grid1", "runtime", "runtime_grid1", "no_ring",
-                              "ring_plain", "ring_plain_grid1"])
+                              "ring_plain", "ring_plain_grid1", "psyn_wide_all", "psyn_plain_grid1"])
 @pytest.mark.parametrize("k,m", PRESETS)
 def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
     """QuicR's negotiated configurations with 1350-byte payloads (bb = 1352): odd k puts every
@@ -786,9 +787,10 @@ def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
         assert "gf_apply" not in fec.last_kernels()
 
 
+@pytest.mark.parametrize("wide", [0, 2])
 @pytest.mark.parametrize("grid", [1, 2, 0])
 @pytest.mark.parametrize("k,m", sorted(PSYN))
-def test_psyn_decode_patterns(tuned_engine, oracle, k, m, grid):
+def test_psyn_decode_patterns(tuned_engine, oracle, k, m, grid, wide):
     """The preset decode (gf_psyn: syndromes of every parity row with the compiled code,
     Gauss-Jordan replayed on the data) on hand-built receive sets: no loss, 1 .. min(k, m)
     losses with first / scattered / last parity rows in any arrival order (blocks streamed
@@ -799,6 +801,7 @@ def test_psyn_decode_patterns(tuned_engine, oracle, k, m, grid):
     the previous group's stores, up to 16 x 2 x min(k, m) of them)."""
     engine = tuned_engine
     engine.set_option("stream_grid", grid)
+    engine.set_option("psyn_wide", wide)
     bb = 1352
     rmax = min(k, m)
     rng = np.random.default_rng(500 + 7 * k + m + grid)
