@@ -6,6 +6,7 @@
 #   tests                 the whole -m gpu suite
 #   tests:<file|-k expr>  one test file (tests/test_gpu_pp.py) or a -k selection
 #   smoke                 __graft_entry__.smoke()
+#   default               python bench.py (the driver's round-end line)
 #   bench:<W>[:<args>]    bench.py --workload W --verify (W = A B C D), extra args after ':'
 #   quick:<W>[:<args>]    bench.py --workload W, no CPU baseline, no host leg, 10 steps
 #   preset:<k>,<m>        quick bench of a QuicR preset
@@ -32,6 +33,7 @@ for step in "$@"; do
       elif [ -f "$rest" ]; then sel="$rest"
       else sel="tests -k '$rest'"; fi
       specs+=("$tag::900::python -u -m pytest $sel -m gpu -x -q --timeout 120 --timeout-method thread") ;;
+    default) specs+=("default::600::python bench.py") ;;
     smoke)  specs+=("smoke::300::python -c 'import __graft_entry__ as g; g.smoke()'") ;;
     bench)  specs+=("$tag::600::python bench.py --workload $W --verify $extra") ;;
     quick)  specs+=("$tag::300::$quick --workload $W $extra") ;;
