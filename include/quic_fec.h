@@ -85,11 +85,13 @@ QFEC_API int qfec_ctx_create(int device, qfec_ctx **out);
 QFEC_API void qfec_ctx_destroy(qfec_ctx *ctx);
 /* Launch-shape options of one context (the defaults are the measured best):
  * "xor_slots" 2..4, "xor_waves" 1..4, "dma" 0/1, "stream" 0/1, "stream_ring" 4..36,
- * "stream_grid" 0.., "const_enc" 0/1, "stream_static" 0/1, "tile" 0/1,
- * "tile_grid" 0.., "tile_depth" 4/6, "tile_pair" 0/1, "pd" 1..3, "flat" 0/1, "enc_rc" 2/4/8, "prep_lane" 0/1,
- * "host_chunk_mb" 1..4096.  get also reads "cus" (compute units of the device).
- * -2 for an unknown name or a value out of range.  No environment variable changes
- * what the library launches. */
+ * "stream_grid" 0.., "const_enc" 0/1, "stream_static" 0/1 (gf_ring encodes), "ring_wide" 0/1
+ * (their wide parity stores), "dcol" 0/1, "dcol_grid" 0.., "dcol_depth" 6/8, "bsyn" 0/1,
+ * "bsyn_depth" 3/5/7, "psyn" 0/1, "psyn_wide" 0..2 (wide recovered-block stores: none,
+ * (10, 10), every code), "pd" 1..3, "flat" 0/1, "enc_rc" 2/4/8, "prep_lane" 0/1,
+ * "host_chunk_mb" 1..4096, "host_min_groups" 1...  get also reads "cus" (compute units of the
+ * device).  -2 for an unknown name or a value out of range (also for the measured-and-removed
+ * variants of earlier versions).  No environment variable changes what the library launches. */
 QFEC_API int qfec_ctx_set_option(qfec_ctx *ctx, const char *name, int value);
 QFEC_API int qfec_ctx_get_option(qfec_ctx *ctx, const char *name, int *value);
 /* Pre-size every per-(k, m) table and workspace for up to `groups` groups so that later
