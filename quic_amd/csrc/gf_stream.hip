@@ -508,7 +508,7 @@ __device__ __forceinline__ void gf_ring_run(
     static_assert(!DECODE || MC == 0, "decode coefficients are per group");
     static_assert(DECODE || MC == RC, "encode: one output per register set");
     static_assert(FM1 >= SH::pl(0), "block 0 of the next group is prefetched in full");
-    static_assert(NP > R, "a group spans more than the ring");
+    static_assert(SH::pf(K - 1) + R - 1 < 2 * NP, "the frontier stays within the next group");
     const int lane = threadIdx.x & 63;
     const int w = wave_id();
     uint8_t* ring = smem + (size_t)w * RB;
@@ -919,7 +919,7 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     // the static ring schedule is used for the encode only: its rolled decode measured
     // slower than gf_stream's (0.644 vs 0.619 ms on config B)
     const bool ring_shape = (k == 32 && m == 4) || (k == 10 && (m == 10 || m == 15 || m == 20)) ||
-                            (k == 250 && m == 5) || (k == 15 && m == 15);
+                            (k == 250 && m == 5) || (k == 15 && m == 15) || (k == 5 && m == 5);
     if (t.stream_static && !decode && s == 169 && ring_shape && t.const_enc) {
         // the fixed B/C shape and the even-k QuicR presets: compile-time ring schedule
         // (gf_ring_kernel)
@@ -953,6 +953,7 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
             case 10 * 256 + 15: note_kernel("gf_ring_kernel<encode,k10m15>"); QR_GO(10, 15); break;
             case 250 * 256 + 5: note_kernel("gf_ring_kernel<encode,k250m5>"); QR_GO(250, 5); break;
             case 15 * 256 + 15: note_kernel("gf_ring_kernel<encode,k15m15>"); QR_GO(15, 15); break;
+            case 5 * 256 + 5: note_kernel("gf_ring_kernel<encode,k5m5>"); QR_GO(5, 5); break;
             default: note_kernel("gf_ring_kernel<encode,k10m20>"); QR_GO1(10, 20, false); break;
         }
 #undef QR_GO

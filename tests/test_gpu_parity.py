@@ -743,7 +743,7 @@ PRESETS = [(5, 5), (10, 10), (10, 15), (10, 20), (15, 15), (250, 5)]   # quic_fe
 
 
 PSYN = {(10, 10), (10, 15), (10, 20), (15, 15)}   # m >= 7: gf_psyn's compiled syndrome decode
-RING_ENC = {(10, 10), (10, 15), (10, 20), (15, 15), (250, 5)}   # gf_ring's static schedule
+RING_ENC = {(5, 5), (10, 10), (10, 15), (10, 20), (15, 15), (250, 5)}   # gf_ring's schedule
 
 
 @pytest.mark.parametrize("opts", [{}, {"stream_grid": 1}, {"psyn": 0},
@@ -756,9 +756,9 @@ RING_ENC = {(10, 10), (10, 15), (10, 20), (15, 15), (250, 5)}   # gf_ring's stat
 def test_reference_presets_stream(tuned_engine, oracle, k, m, opts):
     """QuicR's negotiated configurations with 1350-byte payloads (bb = 1352): odd k puts every
     other group 8 bytes off a 16-byte boundary, m > 8 and more than 8 losses cut the run-time
-    decode's outputs into chunks.  Encodes run gf_ring's static schedule for every preset but
-    (5, 5) (gf_stream with stream_static = 0; odd k streams every other group 8 bytes into
-    its 16-byte aligned stream) and the compiled gf_stream for (5, 5);
+    decode's outputs into chunks.  Encodes run gf_ring's static schedule for every preset
+    (gf_stream with stream_static = 0; odd k streams every other group 8 bytes into its
+    16-byte aligned stream);
     decodes run gf_psyn
     (compiled syndromes + Gauss-Jordan) for the m >= 7 presets and gf_stream for the others,
     never gf_apply; with psyn = 0, the run-time gf_stream decode (nibble-jump products) for
