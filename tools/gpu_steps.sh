@@ -14,7 +14,7 @@
 #   abold:<W>[:<args>]    quick bench against quic_amd/libquic_fec_abold.so (an A/B build)
 #   aboldp:<k>,<m>        the same for a QuicR preset
 #   pmc:<W>[:<args>]      tools/pmc.sh passes (FETCH/WRITE traffic, waves, issue mix)
-# Extra args use '+' for spaces: quick:B:--opt+ring_nt=0.  GPU_STEPS_DRY=1 prints the steps.
+# Extra args use '+' for spaces: quick:B:--opt+bsyn_depth=3.  GPU_STEPS_DRY=1 prints the steps.
 export TMPDIR=/tmp
 specs=()
 tags=()
