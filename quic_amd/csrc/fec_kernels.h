@@ -34,7 +34,7 @@ struct Tune {
     int prep_lane = 1;        // decode prep with 4 lanes per group when it applies
     int bsyn = 1;             // (32, 4) x 1352 B decode: compiled syndrome kernel gf_bsyn
                               //   (0: the run-time gf_stream decode)
-    int bsyn_depth = 5;       // gf_bsyn: blocks in flight per wave (3..7)
+    int bsyn_depth = 3;       // gf_bsyn: blocks in flight per wave (3, 5, 7; 3: 5 waves/SIMD)
     int psyn = 1;             // QuicR presets with m >= 7 at 1352 B: compiled syndrome decode
                               //   gf_psyn (0: the run-time gf_stream decode)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16
