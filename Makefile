@@ -101,12 +101,12 @@ $(ROOT)build/gf_psyn_%.o: $(CSRC)/gf_psyn_%.hip $(CSRC)/gf_psyn.h $(CSRC)/gf_win
 	$(HIPCC) $(HIPFLAGS) $(PSYNFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }
 
-$(ROOT)build/gf_dcol.o: $(CSRC)/gf_dcol.hip $(CSRC)/gf_dcol.h $(HDRS) $(GEN)
+$(ROOT)build/gf_dcol.o: $(CSRC)/gf_dcol.hip $(CSRC)/gf_dcol.h $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }
 
-$(ROOT)build/gf_dcol_%.o: $(CSRC)/gf_dcol_%.hip $(CSRC)/gf_dcol.h $(HDRS) $(GEN)
+$(ROOT)build/gf_dcol_%.o: $(CSRC)/gf_dcol_%.hip $(CSRC)/gf_dcol.h $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }

@@ -70,14 +70,19 @@ QFEC_API int cauchy_256_decode(int k, int m, Block *blocks, int block_bytes);
  * `stream` is a hipStream_t (NULL = HIP's null stream, as everywhere in HIP).  Device
  * entry points only enqueue work on that stream; they do not synchronise.
  *
- * Streams and contexts: a context may be used from several streams.  Its decode
- * workspace is shared by its calls, so the library orders a decode behind the previous
- * decode of the same context when they are enqueued on different streams (an event, not
- * a host wait); calls on one stream are ordered by the stream.  Independent contexts
- * (one per stream, or one per device) share nothing and run concurrently.  While a
- * stream is capturing into a HIP graph the cross-stream ordering is not added: capture
- * the calls of one context on one stream.  Calls on one context are serialised on the
- * host by a mutex (the reference codec is single-threaded per connection).
+ * Streams and contexts: a context may be used from several streams.  Its eager decodes
+ * share one workspace, so the library orders a decode behind the previous eager decode of
+ * the same context when they are enqueued on different streams (an event, not a host
+ * wait); calls on one stream are ordered by the stream.  Decodes captured into a HIP graph
+ * use a second workspace of the context, so a graph replay, on whatever stream it is
+ * launched, never races an eager call.  Graphs captured on one context share that second
+ * workspace: replay them in one stream order (or capture on separate contexts), and capture
+ * the calls of one context on one stream.  A capture allocates nothing when qfec_reserve
+ * covered its batch; a workspace outgrown by a later capture stays allocated until the
+ * context is destroyed, so earlier graphs stay valid.  Independent contexts (one per
+ * stream, or one per device) share nothing and run concurrently.  Calls on one context are
+ * serialised on the host by a mutex (the reference codec is single-threaded per
+ * connection).
  * ------------------------------------------------------------------------------- */
 typedef struct qfec_ctx qfec_ctx;
 
@@ -94,8 +99,9 @@ QFEC_API void qfec_ctx_destroy(qfec_ctx *ctx);
  * variants of earlier versions).  No environment variable changes what the library launches. */
 QFEC_API int qfec_ctx_set_option(qfec_ctx *ctx, const char *name, int value);
 QFEC_API int qfec_ctx_get_option(qfec_ctx *ctx, const char *name, int *value);
-/* Pre-size every per-(k, m) table and workspace for up to `groups` groups so that later
- * calls allocate nothing (required before capturing calls into a HIP graph). */
+/* Pre-size every per-(k, m) table and both decode workspaces (eager and graph) for up to
+ * `groups` groups so that later calls allocate nothing (call it before capturing calls
+ * into a HIP graph). */
 QFEC_API int qfec_reserve(qfec_ctx *ctx, int k, int m, int block_bytes, long long groups);
 
 QFEC_API int qfec_encode_batch(qfec_ctx *ctx, int k, int m, int block_bytes, long long groups,
@@ -234,7 +240,9 @@ QFEC_API int qfec_open_decode_batch(qfec_ctx *ctx, int k, int m, int block_bytes
  * arrays (NULL where the `_all` scalar applies, except h_pkt_len).  Row strides must be > 0.
  *   qfec_encode_seal_groups_batch_host: data [G][k][bb] -> every packet of each group sealed,
  *     h_pkt [G*(k+m)][pkt_stride], h_pkt_len [G*(k+m)] (qfec_encode_seal_groups_batch); the
- *     bytes of a packet row past h_pkt_len[p] are unspecified (staging rows are copied whole);
+ *     bytes of a packet row past h_pkt_len[p] are zero (rows are copied back whole); -1 with
+ *     nothing written where the encode returns -1 (m > 1, k > 1 and (k + m > 256 or
+ *     block_bytes % 8 != 0));
  *   qfec_open_decode_batch_host: wire packets -> h_rec [G][min(k,m)][bb], h_rec_rows,
  *     h_status [G] (may be NULL) and h_open_len [G*(k+m)] (may be NULL)
  *     (qfec_open_decode_batch). */

@@ -143,14 +143,35 @@ struct HostBuf {
 
 }  // namespace
 
+// One decode workspace: the prep's per-group tables and the in-place scratch.
+struct Workspace {
+    DevBuf dcoef, dslots, dnout, dscratch;
+    // graph workspace: a buffer outgrown by a later capture is kept (not freed) until the
+    // context is destroyed, since the graphs captured before still name it
+    bool keep = false;
+    std::vector<std::unique_ptr<DevBuf>> retired;
+    hipError_t ensure(DevBuf& b, size_t bytes) {
+        if (bytes <= b.n) return hipSuccess;
+        if (keep && b.p) {
+            auto old = std::make_unique<DevBuf>();
+            std::swap(old->p, b.p);
+            std::swap(old->n, b.n);
+            retired.push_back(std::move(old));
+        }
+        return b.ensure(bytes);
+    }
+};
+
 struct qfec_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     qfec::Tune tune;
-    // The decode workspace (dcoef, dslots, dnout, dscratch) is one per context.  Calls may
-    // enqueue on any stream: every eager use records ws_ev after its kernels, and a use on
-    // another stream waits for it, so uses of the workspace are ordered across streams
-    // (ws_begin / ws_end).
+    // Decode workspaces.  Eager calls share `ws`; they may enqueue on any stream: every
+    // eager use records ws_ev after its kernels, and a use on another stream waits for it, so
+    // eager uses are ordered across streams (ws_begin / ws_end).  Calls captured into a graph
+    // use `ws_graph` instead, so a replay (on whatever stream it is launched) never shares
+    // tables with an eager call; graphs captured on one context share ws_graph, so their
+    // replays must be ordered with each other (include/quic_fec.h).
     hipEvent_t ws_ev = nullptr;      // on ws_helper, after the last eager use
     hipEvent_t ws_tmp = nullptr;     // on the last eager use's stream
     hipStream_t ws_helper = nullptr;
@@ -159,7 +180,7 @@ struct qfec_ctx {
     // encode coefficient tables keyed by (k, m, rc): [nchunk][k][rcp]; decode cenc by (k, m)
     std::map<std::tuple<int, int, int>, std::unique_ptr<DevBuf>> enc_tab;
     std::map<std::pair<int, int>, std::unique_ptr<DevBuf>> cenc_tab;
-    DevBuf dcoef, dslots, dnout, dscratch;
+    Workspace ws, ws_graph;
     HostBuf h_stage;
     DevBuf d_stage;
     // host-pointer batches: copy-in / copy-out streams around `stream` (compute), NB
@@ -211,6 +232,14 @@ int ws_end(qfec_ctx* c, hipStream_t st) {
     return 0;
 }
 
+// The workspace of a call on `st`: the graph workspace while `st` is capturing.
+Workspace& ws_for(qfec_ctx* c, hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        return c->ws_graph;
+    return c->ws;
+}
+
 // A stream argument is a plain hipStream_t: NULL is HIP's null (default) stream, as
 // everywhere in HIP, so calls order with the caller's other work on that stream.
 hipStream_t pick(qfec_ctx*, void* s) { return (hipStream_t)s; }
@@ -254,15 +283,15 @@ int get_cenc(qfec_ctx* c, int k, int m, const uint8_t** out) {
     return 0;
 }
 
-int decode_workspace(qfec_ctx* c, int k, int rmax, int rc, long long groups) {
+int decode_workspace(Workspace& W, int k, int rmax, int rc, long long groups) {
     const int rcp = std::max(rc, 4);
     const int nchunk = (rmax + rc - 1) / rc;
     // per group: the apply coefficients, or a syndrome table (bsyn:: / syn::)
     const size_t per = std::max<size_t>({(size_t)nchunk * k * rcp, (size_t)qfec::bsyn::kBytes,
                                          (size_t)qfec::psyn::kBytes});
-    QF_HIP(c->dcoef.ensure((size_t)groups * per));
-    QF_HIP(c->dslots.ensure((size_t)groups * rmax));
-    QF_HIP(c->dnout.ensure((size_t)groups * sizeof(int32_t)));
+    QF_HIP(W.ensure(W.dcoef, (size_t)groups * per));
+    QF_HIP(W.ensure(W.dslots, (size_t)groups * rmax));
+    QF_HIP(W.ensure(W.dnout, (size_t)groups * sizeof(int32_t)));
     return 0;
 }
 
@@ -315,10 +344,11 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
         QF_HIP(qfec::launch_rows_k1(d_rows_in, d_rows_out, d_status, G, st));
         return 0;
     }
+    Workspace& W = ws_for(c, st);
     if (m == 1) {   // :1264-1267
-        QF_HIP(c->dslots.ensure((size_t)G));
+        QF_HIP(W.ensure(W.dslots, (size_t)G));
         QF_HIP(qfec::launch_xor_decode(d_blocks, d_out, d_rows_in, d_rows_out, d_status,
-                                       (uint8_t*)c->dslots.p, k, bb, G, st, c->tune));
+                                       (uint8_t*)W.dslots.p, k, bb, G, st, c->tune));
         return 0;
     }
     const int rmax = std::min(k, m);
@@ -327,8 +357,8 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     const uint8_t* cenc = nullptr;
     int r = get_cenc(c, k, m, &cenc);
     if (r) return r;
-    if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
-    qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
+    if ((r = decode_workspace(W, k, rmax, rc, G))) return r;
+    qfec::DecodeWork w{(uint8_t*)W.dcoef.p, (uint8_t*)W.dslots.p, (int32_t*)W.dnout.p};
     const long long tab_gstride = (long long)nchunk * k * std::max(rc, 4);
     const bool dcol = qfec::gf_dcol_supported(k, m, bb, c->tune) && rmax <= 16;
     if (dcol && ((uintptr_t)d_blocks & 15) == 0) {
@@ -375,21 +405,21 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
         }
         // in place with several chunks: the recovered blocks go to scratch first, then to
         // their slots (a later chunk reads slots an earlier one would have overwritten)
-        QF_HIP(c->dscratch.ensure((size_t)G * rmax * bb));
-        QF_HIP(qfec::launch_gf_stream(d_blocks, (uint8_t*)c->dscratch.p, w.coef, nullptr, w.nout,
+        QF_HIP(W.ensure(W.dscratch, (size_t)G * rmax * bb));
+        QF_HIP(qfec::launch_gf_stream(d_blocks, (uint8_t*)W.dscratch.p, w.coef, nullptr, w.nout,
                                       k, m, bb, G, rc, rmax, (long long)nchunk * k * rcp,
                                       (long long)rmax * bb, true, st, c->tune));
-        QF_HIP(qfec::launch_scatter_recovered((const uint8_t*)c->dscratch.p, d_out, w, k, bb,
+        QF_HIP(qfec::launch_scatter_recovered((const uint8_t*)W.dscratch.p, d_out, w, k, bb,
                                               rmax, G, st));
         return 0;
     }
     if (nchunk > 1 && d_out == d_blocks) {
         // in place with several output chunks: a later chunk would read slots an earlier
         // chunk already overwrote, so stage the recovered blocks first
-        QF_HIP(c->dscratch.ensure((size_t)G * rmax * bb));
-        QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, (uint8_t*)c->dscratch.p, w, k, m, bb, G,
+        QF_HIP(W.ensure(W.dscratch, (size_t)G * rmax * bb));
+        QF_HIP(qfec::launch_gf_decode_scratch(d_blocks, (uint8_t*)W.dscratch.p, w, k, m, bb, G,
                                               rc, rmax, st, c->tune));
-        QF_HIP(qfec::launch_scatter_recovered((const uint8_t*)c->dscratch.p, d_out, w, k, bb,
+        QF_HIP(qfec::launch_scatter_recovered((const uint8_t*)W.dscratch.p, d_out, w, k, bb,
                                               rmax, G, st));
         return 0;
     }
@@ -422,18 +452,19 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
                                    st));
         return 0;
     }
+    Workspace& W = ws_for(c, st);
     if (m == 1) {
-        QF_HIP(c->dslots.ensure((size_t)G));
+        QF_HIP(W.ensure(W.dslots, (size_t)G));
         QF_HIP(qfec::launch_xor_decode(d_blocks, d_rec, d_rows_in, d_rec_rows, d_status,
-                                       (uint8_t*)c->dslots.p, k, bb, G, st, c->tune, true));
+                                       (uint8_t*)W.dslots.p, k, bb, G, st, c->tune, true));
         return 0;
     }
     const int rc = stream_decode_rc(rmax);
     const uint8_t* cenc = nullptr;
     int r = get_cenc(c, k, m, &cenc);
     if (r) return r;
-    if ((r = decode_workspace(c, k, rmax, rc, G))) return r;
-    qfec::DecodeWork w{(uint8_t*)c->dcoef.p, (uint8_t*)c->dslots.p, (int32_t*)c->dnout.p};
+    if ((r = decode_workspace(W, k, rmax, rc, G))) return r;
+    qfec::DecodeWork w{(uint8_t*)W.dcoef.p, (uint8_t*)W.dslots.p, (int32_t*)W.dnout.p};
     const bool dcol = qfec::gf_dcol_supported(k, m, bb, c->tune) && rmax <= 16;
     if (dcol && ((uintptr_t)d_blocks & 15) == 0) {
         const int nchunk = (rmax + rc - 1) / rc;
@@ -728,6 +759,7 @@ int qfec_ctx_create(int device, qfec_ctx** out) {
     if (device < 0 || device >= n) return fail(-2, "no such HIP device");
     auto c = std::make_unique<qfec_ctx>();
     c->device = device;
+    c->ws_graph.keep = true;
     QF_HIP(hipSetDevice(device));
     int cus = 0;
     QF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -743,8 +775,9 @@ void qfec_ctx_destroy(qfec_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     // the last use of the workspace may be on any stream the caller used (and may have
-    // destroyed since): wait for the whole device rather than for a stored stream handle
-    if (c->ws_used) (void)hipDeviceSynchronize();
+    // destroyed since), and a graph replay may still read the graph workspace: wait for the
+    // whole device rather than for a stored stream handle
+    if (c->ws_used || c->ws_graph.dslots.p) (void)hipDeviceSynchronize();
     for (hipStream_t s : {c->stream, c->s_in, c->s_out})
         if (s) (void)hipStreamSynchronize(s);
     if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
@@ -994,6 +1027,10 @@ int qfec_encode_seal_groups_batch_host(qfec_ctx* c, int k, int m, int bb, long l
     if (groups == 0) return 0;
     if (hdr_stride <= 0 && h_hdr) return fail(-2, "host headers need a row stride > 0");
     if (pkt_stride <= 0) return fail(-2, "host packets need a row stride > 0");
+    // the encode's -1 (cauchy_256.cpp:1530-1534): no packet is sealed, as on the device path
+    // (the parity rows past P0 would be stale staging bytes sent with valid tags)
+    if (m > 1 && k > 1 && (k + m > 256 || bb % 8 != 0))
+        return fail(-1, "unsupported (k + m > 256 or block_bytes % 8 != 0)");
     std::lock_guard<std::mutex> lk(c->mu);
     if ((rc = set_device(c))) return rc;
     const long long np = k + m;                        // packets per group
@@ -1002,7 +1039,6 @@ int qfec_encode_seal_groups_batch_host(qfec_ctx* c, int k, int m, int bb, long l
     const size_t pkt_g = (size_t)np * pkt_stride;
     const size_t len_g = (size_t)np * sizeof(int32_t);
     const size_t per = in_g + par_g + hdr_g + pkt_g + len_g * (1 + (h_hdr_len ? 1 : 0) + (h_pt_len ? 1 : 0));
-    int result = 0;
     rc = host_pipeline(c, groups, per, [&](long long g0, long long n, uint8_t* buf,
                                            int phase) -> int {
         Carve cv{buf};
@@ -1028,8 +1064,11 @@ int qfec_encode_seal_groups_batch_host(qfec_ctx* c, int k, int m, int bb, long l
                                       hipMemcpyHostToDevice, c->s_in));
         } else if (phase == 1) {
             const int r = encode_impl(c, k, m, bb, n, dd, dp, c->stream);
-            if (r < -1) return r;
-            if (r) result = r;
+            if (r) return r;
+            // packet rows are copied back whole: zero the staging rows first, so the bytes of
+            // a row past its packet are zeros (as the device path leaves them untouched), not
+            // an earlier chunk's packets
+            QF_HIP(hipMemsetAsync(dk, 0, pn * pkt_stride, c->stream));
             QF_HIP(qfec::launch_null_seal_groups(k, m, bb, n, dd, dp, dh,
                                                  dh ? hdr_stride : 0, dhl, dh ? hdr_len_all : 0,
                                                  dpl, pt_len_all, dk, pkt_stride, dkl, c->stream));
@@ -1041,7 +1080,7 @@ int qfec_encode_seal_groups_batch_host(qfec_ctx* c, int k, int m, int bb, long l
         }
         return 0;
     }, kCarveSlack);
-    return rc ? rc : result;
+    return rc;
 }
 
 // Receiver, host memory to host memory: wire packets in, the recovered blocks (and, if asked,
@@ -1275,7 +1314,15 @@ int qfec_reserve(qfec_ctx* c, int k, int m, int bb, long long groups) {
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(c->mu);
     if ((rc = set_device(c))) return rc;
-    QF_HIP(c->dslots.ensure((size_t)groups));   // m == 1 decode: erased slot per group
+    // both workspaces: the eager one and the one calls captured into a graph use
+    for (Workspace* W : {&c->ws, &c->ws_graph}) {
+        QF_HIP(W->ensure(W->dslots, (size_t)groups));   // m == 1 decode: erased slot per group
+        if (m > 1 && k > 1) {
+            const int rmax = std::min(k, m);
+            if ((rc = decode_workspace(*W, k, rmax, decode_rc(rmax), groups))) return rc;
+            if (rmax > decode_rc(rmax)) QF_HIP(W->ensure(W->dscratch, (size_t)groups * rmax * bb));
+        }
+    }
     if (m > 1 && k > 1 && k + m <= 256) {
         const uint8_t* t;
         if ((rc = get_enc_table(c, k, m, stream_encode_rc(k, m, bb, true, c->tune), &t))) return rc;
@@ -1283,9 +1330,6 @@ int qfec_reserve(qfec_ctx* c, int k, int m, int bb, long long groups) {
     if (m > 1 && k > 1) {
         const uint8_t* t;
         if ((rc = get_cenc(c, k, m, &t))) return rc;
-        const int rmax = std::min(k, m);
-        if ((rc = decode_workspace(c, k, rmax, decode_rc(rmax), groups))) return rc;
-        if (rmax > decode_rc(rmax)) QF_HIP(c->dscratch.ensure((size_t)groups * rmax * bb));
     }
     return 0;
 }

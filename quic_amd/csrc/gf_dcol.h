@@ -47,6 +47,7 @@
 #include "cauchy_const.h"
 #include "fec_kernels.h"
 #include "gf_bitslice.h"
+#include "gf_winjump.h"
 
 namespace qfec {
 
@@ -315,6 +316,17 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void gf_dcol_kernel(
         const uint8_t* tb = tab + (DECODE ? g * tab_gstride : 0);
         make_unit(i + 1, nu, vn0, vn1);
         rows_start(nu, rn_n);
+        // decode: the syndrome rows the solve uses (the received parity rows, syn::kNeed) and
+        // the present data rows (syn::kMask); rows outside them are skipped by uniform
+        // branches (cauchy_256.cpp:712-795: only received recovery rows enter the system)
+        uint32_t need = 0xFFFFu, pm0 = ~0u, pm1 = ~0u, pm2 = ~0u, pm3 = ~0u;
+        if constexpr (DECODE) {
+            need = dc_cload_u32(tb, syn::kNeed);
+            pm0 = dc_cload_u32(tb, syn::kMask);
+            pm1 = dc_cload_u32(tb, syn::kMask + 4);
+            pm2 = dc_cload_u32(tb, syn::kMask + 8);
+            pm3 = dc_cload_u32(tb, syn::kMask + 12);
+        }
         uint32_t acc[RW][8];
 #pragma unroll
         for (int y = 0; y < RW; ++y)
@@ -335,13 +347,31 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void gf_dcol_kernel(
             }
             uint32_t w8[8];
             next_block(std::bool_constant<(x + 1 <= D - 1)>{}, nlo, nhi);
-            realign(lo, hi, w8);
-            Win win;
-            win_build(w8, win);
-            static_for<RW>([&](auto yc) __attribute__((always_inline)) {
-                constexpr int y = decltype(yc)::value;
-                win_apply<cauchy_coef(MC, y, x)>(acc[y], win);
-            });
+            if constexpr (DECODE) {
+                // an erased row's zero block adds nothing; a row the solve does not use is
+                // not accumulated (the empty asm keeps each branch a branch: no select)
+                const uint32_t pw = x < 32 ? pm0 : x < 64 ? pm1 : x < 96 ? pm2 : pm3;
+                if (__builtin_expect((pw >> (x % 32)) & 1u, 1)) {
+                    realign(lo, hi, w8);
+                    Win win;
+                    win_build(w8, win);
+                    static_for<RW>([&](auto yc) __attribute__((always_inline)) {
+                        constexpr int y = decltype(yc)::value;
+                        if (__builtin_expect((need >> y) & 1u, 1)) {
+                            asm volatile("");
+                            win_apply<cauchy_coef(MC, y, x)>(acc[y], win);
+                        }
+                    });
+                }
+            } else {
+                realign(lo, hi, w8);
+                Win win;
+                win_build(w8, win);
+                static_for<RW>([&](auto yc) __attribute__((always_inline)) {
+                    constexpr int y = decltype(yc)::value;
+                    win_apply<cauchy_coef(MC, y, x)>(acc[y], win);
+                });
+            }
         };
         static_for<KC>([&](auto xc) __attribute__((always_inline)) {
             // accumulators opaque at every block boundary: with constant coefficients the XOR
@@ -412,9 +442,11 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void gf_dcol_kernel(
                     expand_wz(v);
                     static_for<MC>([&](auto yc) __attribute__((always_inline)) {
                         constexpr int yy = decltype(yc)::value;
-                        const uint32_t cf = (uint32_t)dc_cload_u8(cenc, yy * KC + row);
-                        apply_nibble<0>(acc[yy], cf & 15u, v);
-                        apply_nibble<4>(acc[yy], cf >> 4, v);
+                        if ((need >> yy) & 1u) {
+                            const uint32_t cf = (uint32_t)dc_cload_u8(cenc, yy * KC + row);
+                            apply_nibble<0>(acc[yy], cf & 15u, v);
+                            apply_nibble<4>(acc[yy], cf >> 4, v);
+                        }
                     });
                 }
             };
@@ -461,9 +493,10 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void gf_dcol_kernel(
                     for (int q = 0; q < PO; ++q) {
                         const int j = PO * ps + q;
                         if (j < n) {
+                            // nibble jumps (gf_winjump.h): one indirect jump per nibble
+                            // instead of a 16-way branch tree
                             const uint32_t cf = (uint32_t)dc_cload_u8(tb, syn::kSinv + j * 16 + ii);
-                            apply_nibble<0>(o[q], cf & 15u, v);
-                            apply_nibble<4>(o[q], cf >> 4, v);
+                            wz_mul_acc_rt(o[q], v, cf);
                         }
                     }
                 }

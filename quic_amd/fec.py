@@ -305,9 +305,36 @@ def _hptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _hcheck(t, name, dtype, shape):
+    """A host buffer argument: a contiguous CPU tensor of `dtype` and exactly `shape` (None in
+    `shape`: any extent, > 0).  The library copies whole rows into and out of it, so a short
+    buffer would be overrun and a wrong dtype misread: ValueError / TypeError instead."""
+    import torch
+    if not isinstance(t, torch.Tensor) or t.is_cuda or not t.is_contiguous():
+        raise TypeError(f"{name}: host buffers must be contiguous CPU tensors "
+                        "(pinned for full speed)")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if t.dim() != len(shape) or any(want is not None and got != want
+                                    for got, want in zip(t.shape, shape)) \
+            or any(got <= 0 for got, want in zip(t.shape, shape) if want is None):
+        raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+
+
+def _hcheck_lens(lens, name, n):
+    """A per-packet length argument: an int (the same for every packet) or int32 [n]."""
+    import torch
+    if not isinstance(lens, int):
+        _hcheck(lens, name, torch.int32, (n,))
+
+
 def encode_host_into(engine, k, m, block_bytes, data_h, parity_h):
     """Host-pointer encode on caller-owned CPU tensors (pinned memory recommended):
     H2D, kernels and D2H pipelined in chunks inside the library.  Returns 0 / -1."""
+    import torch
+    G = data_h.shape[0]
+    _hcheck(data_h, "data", torch.uint8, (G, k, block_bytes))
+    _hcheck(parity_h, "parity", torch.uint8, (G, m, block_bytes))
     rc = engine.lib.qfec_encode_batch_host(engine._h, k, m, block_bytes, data_h.shape[0],
                                            _hptr(data_h), _hptr(parity_h))
     if rc < -1:
@@ -318,6 +345,12 @@ def encode_host_into(engine, k, m, block_bytes, data_h, parity_h):
 def decode_host_into(engine, k, m, block_bytes, blocks_h, rows_h, status_h=None):
     """Host-pointer in-place decode on caller-owned CPU tensors (cauchy_256_decode
     semantics per group)."""
+    import torch
+    G = blocks_h.shape[0]
+    _hcheck(blocks_h, "blocks", torch.uint8, (G, k, block_bytes))
+    _hcheck(rows_h, "rows", torch.uint8, (G, k))
+    if status_h is not None:
+        _hcheck(status_h, "status", torch.int32, (G,))
     rc = engine.lib.qfec_decode_batch_host(engine._h, k, m, block_bytes, blocks_h.shape[0],
                                            _hptr(blocks_h), _hptr(rows_h),
                                            None if status_h is None else _hptr(status_h))
@@ -339,6 +372,16 @@ def encode_seal_groups_host_into(engine, k, m, block_bytes, data_h, hdr_h, hdr_l
     """Sender, host to host (qfec_encode_seal_groups_batch_host): data [G][k][bb] and
     headers hdr [G*(k+m)][hdr_stride] (or None) -> every packet sealed into pkt
     [G*(k+m)][pkt_stride], pkt_len int32 [G*(k+m)].  Returns 0 / -1."""
+    import torch
+    G = data_h.shape[0]
+    n = G * (k + m)
+    _hcheck(data_h, "data", torch.uint8, (G, k, block_bytes))
+    if hdr_h is not None:
+        _hcheck(hdr_h, "hdr", torch.uint8, (n, None))
+    _hcheck_lens(hdr_len, "hdr_len", n)
+    _hcheck_lens(pt_len, "pt_len", n)
+    _hcheck(pkt_h, "pkt", torch.uint8, (n, None))
+    _hcheck(pkt_len_h, "pkt_len", torch.int32, (n,))
     h, h_all = _hlens(hdr_len)
     p, p_all = _hlens(pt_len)
     rc = engine.lib.qfec_encode_seal_groups_batch_host(
@@ -355,6 +398,18 @@ def open_decode_host_into(engine, k, m, block_bytes, pkt_h, pkt_len_h, ad_len, r
     """Receiver, host to host (qfec_open_decode_batch_host): wire packets pkt
     [G*(k+m)][stride], pkt_len int32 (< 0: not received) -> rec [G][min(k,m)][bb],
     rec_rows, status [G], open_len [G*(k+m)]."""
+    import torch
+    G = rec_h.shape[0]
+    n, rmax = G * (k + m), min(k, m)
+    _hcheck(pkt_h, "pkt", torch.uint8, (n, None))
+    _hcheck(pkt_len_h, "pkt_len", torch.int32, (n,))
+    _hcheck_lens(ad_len, "ad_len", n)
+    _hcheck(rec_h, "rec", torch.uint8, (G, rmax, block_bytes))
+    _hcheck(rec_rows_h, "rec_rows", torch.uint8, (G, rmax))
+    if status_h is not None:
+        _hcheck(status_h, "status", torch.int32, (G,))
+    if open_len_h is not None:
+        _hcheck(open_len_h, "open_len", torch.int32, (n,))
     a, a_all = _hlens(ad_len)
     rc = engine.lib.qfec_open_decode_batch_host(
         engine._h, k, m, block_bytes, rec_h.shape[0], _hptr(pkt_h), pkt_h.stride(0),
@@ -369,6 +424,14 @@ def open_decode_host_into(engine, k, m, block_bytes, pkt_h, pkt_len_h, ad_len, r
 def decode_recovered_host_into(engine, k, m, block_bytes, blocks_h, rows_h, rec_h, rec_rows_h,
                                status_h=None):
     """Host-pointer decode returning only the recovered blocks (CPU tensors)."""
+    import torch
+    G, rmax = blocks_h.shape[0], min(k, m)
+    _hcheck(blocks_h, "blocks", torch.uint8, (G, k, block_bytes))
+    _hcheck(rows_h, "rows", torch.uint8, (G, k))
+    _hcheck(rec_h, "rec", torch.uint8, (G, rmax, block_bytes))
+    _hcheck(rec_rows_h, "rec_rows", torch.uint8, (G, rmax))
+    if status_h is not None:
+        _hcheck(status_h, "status", torch.int32, (G,))
     rc = engine.lib.qfec_decode_batch_recovered_host(
         engine._h, k, m, block_bytes, blocks_h.shape[0], _hptr(blocks_h), _hptr(rows_h),
         _hptr(rec_h), _hptr(rec_rows_h), None if status_h is None else _hptr(status_h))

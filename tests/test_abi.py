@@ -177,3 +177,52 @@ def test_grouped_packet_entry_points_reject_bad_arguments():
     assert L.qfec_encode_seal_groups_batch(None, *args_seal) == -2
     assert L.qfec_open_decode_batch(None, 10, 1, 1352, 0, None, 1400, None, None, 16, None,
                                     None, None, None, None, None, None) == -2
+
+
+def test_host_buffer_arguments_checked_before_the_call():
+    """The host-to-host wrappers check every buffer's dtype and row count before the library
+    call: the library copies whole rows into and out of them, so a short packet
+    or length buffer would be overrun and an int64 length array misread.  The engine is never
+    touched (None), so this runs without a GPU."""
+    import torch
+    k, m, bb, G = 10, 1, 1352, 3
+    n = G * (k + m)
+    u8, i32 = torch.uint8, torch.int32
+    data = torch.zeros((G, k, bb), dtype=u8)
+    hdr = torch.zeros((n, 20), dtype=u8)
+    pkt = torch.zeros((n, 1400), dtype=u8)
+    plen = torch.zeros(n, dtype=i32)
+    bad = [
+        dict(pkt=torch.zeros((n - 1, 1400), dtype=u8)),             # one packet row short
+        dict(plen=torch.zeros(n - 1, dtype=i32)),                    # one length short
+        dict(plen=torch.zeros(n, dtype=torch.int64)),                # int64 lengths
+        dict(hdr_len=torch.zeros(n, dtype=torch.int64)),
+        dict(hdr=torch.zeros((n, 20), dtype=torch.int8)),
+        dict(data=torch.zeros((G, k, bb - 8), dtype=u8)),            # wrong block size
+    ]
+    for b in bad:
+        a = dict(data=data, hdr=hdr, hdr_len=16, pkt=pkt, plen=plen)
+        a.update(b)
+        with pytest.raises(ValueError):
+            fec.encode_seal_groups_host_into(None, k, m, bb, a["data"], a["hdr"], a["hdr_len"],
+                                             bb, a["pkt"], a["plen"])
+    with pytest.raises(TypeError):
+        fec.encode_seal_groups_host_into(None, k, m, bb, data, hdr, 16, bb, pkt[:, ::2], plen)
+    rmax = min(k, m)
+    rec, rr, st = (torch.zeros((G, rmax, bb), dtype=u8), torch.zeros((G, rmax), dtype=u8),
+                   torch.zeros(G, dtype=i32))
+    for b in [dict(plen=torch.zeros(n + 5, dtype=i32)), dict(st=torch.zeros(G, dtype=torch.int64)),
+              dict(rr=torch.zeros((G, rmax + 1), dtype=u8)), dict(ol=torch.zeros(n - 1, dtype=i32))]:
+        a = dict(pkt=pkt, plen=plen, rec=rec, rr=rr, st=st, ol=torch.zeros(n, dtype=i32))
+        a.update(b)
+        with pytest.raises(ValueError):
+            fec.open_decode_host_into(None, k, m, bb, a["pkt"], a["plen"], 16, a["rec"], a["rr"],
+                                      a["st"], a["ol"])
+    blocks, rows = torch.zeros((G, k, bb), dtype=u8), torch.zeros((G, k), dtype=u8)
+    with pytest.raises(ValueError):
+        fec.decode_recovered_host_into(None, k, m, bb, blocks, torch.zeros((G, k - 1), dtype=u8), rec,
+                                       rr, st)
+    with pytest.raises(ValueError):
+        fec.decode_host_into(None, k, m, bb, blocks, rows, torch.zeros(G + 1, dtype=i32))
+    with pytest.raises(ValueError):
+        fec.encode_host_into(None, k, m, bb, data, torch.zeros((G, m + 1, bb), dtype=u8))

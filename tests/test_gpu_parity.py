@@ -931,6 +931,56 @@ def test_workspace_eager_capture_other_stream():
     eng.close()
 
 
+def test_graph_replay_then_eager_other_stream():
+    """A decode captured into a graph on stream A and replayed there, then an eager decode of
+    the same context on stream B: the eager call's prep must not overwrite the
+    tables the replay still reads.  Captured calls use the context's graph workspace, so the
+    two never share tables.  The replay is checked after B's decode has been enqueued."""
+    import torch
+    k, m, bb = 32, 4, 1352
+    eng = fec.FecEngine(0)
+    ga, gb = 65536, 65536
+    eng.reserve(k, m, bb, ga)
+
+    def setup(G, lost, par, seed):
+        gen = torch.Generator(device="cuda").manual_seed(seed)
+        data = torch.randint(0, 256, (G, k, bb), dtype=torch.uint8, device="cuda", generator=gen)
+        parity = torch.empty((G, m, bb), dtype=torch.uint8, device="cuda")
+        eng.encode(k, m, bb, data, parity)
+        recv = data.clone()
+        rows = torch.arange(k, dtype=torch.uint8, device="cuda").repeat(G, 1)
+        for x, y in zip(lost, par):
+            recv[:, x] = parity[:, y]
+            rows[:, x] = k + y
+        rec = torch.full((G, m, bb), 0x5A, dtype=torch.uint8, device="cuda")
+        rr = torch.zeros((G, m), dtype=torch.uint8, device="cuda")
+        st = torch.full((G,), 7, dtype=torch.int32, device="cuda")
+        return data, recv, rows, rec, rr, st
+
+    A = setup(ga, [0, 1, 7, 20], [0, 1, 2, 3], 11)
+    B = setup(gb, [5], [2], 12)
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=sa):
+        eng.decode_recovered(k, m, bb, A[1], A[2], A[3], A[4], A[5], stream=sa.cuda_stream)
+    torch.cuda.synchronize()
+    A[3].fill_(0x5A)
+    A[5].fill_(7)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sa):
+        g.replay()
+    eng.decode_recovered(k, m, bb, B[1], B[2], B[3], B[4], B[5], stream=sb.cuda_stream)
+    torch.cuda.synchronize()
+    for (data, recv, rows, rec, rr, st), lost in ((A, [0, 1, 7, 20]), (B, [5])):
+        assert bool((st == 0).all())
+        srt = sorted(lost)
+        assert bool((rr[:, :len(srt)] == torch.tensor(srt, dtype=torch.uint8, device="cuda")).all())
+        for j, x in enumerate(srt):
+            assert torch.equal(rec[:, j], data[:, x]), (x, j)
+    eng.close()
+
+
 # ------------------------------------------------- gf_bsyn (compiled (32, 4) decode, B/C)
 @pytest.mark.parametrize("depth", [3, 5, 7])
 @pytest.mark.parametrize("grid", [1, 2, 0])

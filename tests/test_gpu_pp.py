@@ -342,9 +342,9 @@ def test_host_protected_paths_vs_oracle(oracle, k, m, G, chunk):
                                           h_pkt, h_len)
     assert rc == 0
     assert np.array_equal(h_len.numpy(), eres)
-    got = h_pkt.numpy()
-    for p in range(n):                       # a row's bytes past its length are unspecified
-        assert np.array_equal(got[p, :eres[p]], exp[p, :eres[p]]), p
+    # whole rows: the bytes past a packet are zero (the staging rows are zeroed before the
+    # seal), as in the oracle's rows, not an earlier chunk's packets
+    assert np.array_equal(h_pkt.numpy(), exp)
     # receiver: lost and tampered packets, one unrecoverable group
     pkt, pkt_len = exp.copy(), eres.copy()
     lost = rng.random(n) < 0.3 * m / per
@@ -434,3 +434,22 @@ def test_grouped_argument_limits(engine):
     with pytest.raises(FecError):
         engine.seal_groups(4, 2, bb, data, par, hdr, 16, bb + 1, out, olen)
     torch.cuda.synchronize()
+
+
+def test_host_seal_unsupported_shape_writes_nothing(oracle):
+    """qfec_encode_seal_groups_batch_host where the encode returns -1 (m > 1 and
+    block_bytes % 8 != 0, cauchy_256.cpp:1530-1534): -1 and no packet written, as on the
+    device path (the parity rows past P0 would otherwise be stale staging bytes sent with
+    valid tags)."""
+    import torch
+    from quic_amd import fec
+    eng = fec.FecEngine(0)
+    k, m, bb, G = 5, 3, 1350, 4
+    n = G * (k + m)
+    data = torch.randint(0, 256, (G, k, bb), dtype=torch.uint8)
+    pkt = torch.full((n, 1400), 0xA5, dtype=torch.uint8)
+    plen = torch.full((n,), 7, dtype=torch.int32)
+    rc = fec.encode_seal_groups_host_into(eng, k, m, bb, data, None, 0, bb, pkt, plen)
+    assert rc == -1
+    assert bool((pkt == 0xA5).all()) and bool((plen == 7).all())
+    eng.close()
