@@ -357,7 +357,10 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void gf_dcol_kernel(
                     win_build(w8, win);
                     static_for<RW>([&](auto yc) __attribute__((always_inline)) {
                         constexpr int y = decltype(yc)::value;
-                        if (__builtin_expect((need >> y) & 1u, 1)) {
+#ifndef QFEC_DCOL_ROWSKIP
+#define QFEC_DCOL_ROWSKIP 1
+#endif
+                        if (!QFEC_DCOL_ROWSKIP || __builtin_expect((need >> y) & 1u, 1)) {
                             asm volatile("");
                             win_apply<cauchy_coef(MC, y, x)>(acc[y], win);
                         }

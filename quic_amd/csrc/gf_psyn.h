@@ -172,6 +172,9 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
         const long long g = g0 + (long long)i * W;
         const uint8_t* tb = tab + g * (long long)psyn::kBytes;
         const uint32_t mlo = psyn_cload_u32(tb, psyn::kMask), mhi = psyn_cload_u32(tb, psyn::kMask + 4);
+        // the syndrome rows the solve uses (the received parity rows); the others are not
+        // accumulated (cauchy_256.cpp:712-795: only received recovery rows enter the system)
+        const uint32_t need = psyn_cload_u32(tb, psyn::kNeed);
         const int n = min(min(nout[g], rmax), RC);
         const int ne = KC - __builtin_popcount(mlo) - __builtin_popcount(mhi);
         int p = 0;    // blocks of this group consumed
@@ -225,7 +228,11 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                 win_build(wv, win);
                 static_for<MC>([&](auto yc) __attribute__((always_inline)) {
                     constexpr int y = decltype(yc)::value;
-                    win_apply<cauchy_coef(MC, y, x)>(acc[y], win);
+                    // a uniform branch per row; the empty asm keeps it a branch (no select)
+                    if (__builtin_expect((need >> y) & 1u, 1)) {
+                        asm volatile("");
+                        win_apply<cauchy_coef(MC, y, x)>(acc[y], win);
+                    }
                 });
             }
         });
@@ -249,6 +256,7 @@ __global__ __launch_bounds__(kPsynWaves * 64) void gf_psyn_kernel(
                 expand_wz(v);
 #pragma unroll 1
                 for (int yy = 0; yy < MC; ++yy) {
+                    if (!((need >> yy) & 1u)) continue;
                     const int ci = yy * KC + row;
                     const uint32_t cf = (psyn_cload_u32(cenc, ci & ~3) >> (8 * (ci & 3))) & 0xFFu;
                     uint32_t tmp[8];
@@ -395,6 +403,7 @@ hipError_t psyn_go_1010(const PsynLaunch& a);
 hipError_t psyn_go_1015(const PsynLaunch& a);
 hipError_t psyn_go_1020(const PsynLaunch& a);
 hipError_t psyn_go_1515(const PsynLaunch& a);
+hipError_t psyn_go_55(const PsynLaunch& a);
 
 // One code's kernel: ring depth 5, no register prefetch, solve products by nibble jumps,
 // non-temporal stores (the other variants measured slower, 3.7).

@@ -237,6 +237,11 @@ __global__ __launch_bounds__(256) void decode_prep_psyn_kernel(
             *(uint32_t*)(T + psyn::kMask + 4) = (uint32_t)(present >> 32);
         }
         if (l < n) T[psyn::kYs + mys] = (uint8_t)myy;
+        // the syndrome rows the solve uses: the kernel accumulates only these
+        uint32_t need = l < n ? 1u << myy : 0u;
+#pragma unroll
+        for (int o = 1; o < kPsynLanes; o <<= 1) need |= (uint32_t)__shfl_xor((int)need, o, kPsynLanes);
+        if (l == 0) *(uint32_t*)(T + psyn::kNeed) = need;
     } else {
         for (int i = l; i < k; i += kPsynLanes) {
             T[psyn::kPerm + i] = (uint8_t)i;
@@ -273,11 +278,15 @@ __global__ __launch_bounds__(256) void decode_prep_psyn_kernel(
 }
 
 // ------------------------------------------------------------------ launchers
-// The codes compiled here: the QuicR presets with m >= 7 (their matrices are column-scaled
-// Cauchy matrices: no pivoting needed), at 1352-byte blocks.
+// The codes compiled here, at 1352-byte blocks: the QuicR presets with m >= 7 (their matrices
+// are column-scaled Cauchy matrices: no pivoting needed) and FEC_5_5, whose 5 x 5 matrix (the
+// ones row and CAUCHY_MATRIX_5's rows, cauchy_256.cpp:428-442) has every square submatrix
+// nonsingular (checked exhaustively by tests/test_psyn_prep.py), so it needs no pivoting
+// either.
 bool gf_psyn_supported(int k, int m, int bb, int rmax, const Tune& t) {
     if (!t.psyn || !t.const_enc || bb != 8 * kPsynS || rmax > 16) return false;
-    return (k == 10 && (m == 10 || m == 15 || m == 20)) || (k == 15 && m == 15);
+    return (k == 10 && (m == 10 || m == 15 || m == 20)) || (k == 15 && m == 15) ||
+           (k == 5 && m == 5);
 }
 
 hipError_t launch_decode_prep_psyn(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
@@ -306,10 +315,11 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
     PsynLaunch a;
     a.in = in, a.out = out, a.tab = tab, a.cenc = cenc, a.slots = slots, a.nout = nout;
     a.groups = groups, a.rmax = rmax, a.out_gstride = out_gstride, a.st = st, a.t = &t, a.k = k;
-    // wide recovered-block stores: measured faster for (10, 10) only (0.370-0.382 -> 0.348-
-    // 0.356 ms; (15, 15) and (10, 20) unchanged, (10, 15) 0.392 -> 0.410), so psyn_wide = 1
-    // (default) takes them there and psyn_wide = 2 for every code; out 8-byte aligned
-    a.wide = (t.psyn_wide == 2 || (t.psyn_wide == 1 && k == 10 && m == 10)) &&
+    // wide recovered-block stores: measured faster for (10, 10) (0.370-0.382 -> 0.348-0.356
+    // ms) and (5, 5) (0.185 -> 0.156 ms); (15, 15) and (10, 20) unchanged, (10, 15) 0.392 ->
+    // 0.410; so psyn_wide = 1 (default) takes them for those two and psyn_wide = 2 for every
+    // code; out 8-byte aligned
+    a.wide = (t.psyn_wide == 2 || (t.psyn_wide == 1 && ((k == 10 && m == 10) || (k == 5 && m == 5)))) &&
              ((((uintptr_t)out) | (uintptr_t)out_gstride) & 7) == 0;
     a.lds = (size_t)kPsynWaves * ((5 + 1) * SH::BUFB + (a.wide ? kPsynStage : 0));   // ring depth 5
     note_kernel("gf_psyn_kernel<decode,preset>");
@@ -317,6 +327,7 @@ hipError_t launch_gf_psyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
         case 10 * 256 + 10: return psyn_go_1010(a);
         case 10 * 256 + 15: return psyn_go_1015(a);
         case 10 * 256 + 20: return psyn_go_1020(a);
+        case 5 * 256 + 5: return psyn_go_55(a);
         default: return psyn_go_1515(a);
     }
 }

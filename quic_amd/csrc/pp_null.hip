@@ -12,18 +12,23 @@
 //        the output holds a copy of the ciphertext before the check and the plaintext after.
 //   FNV-1a-128 (quic_utils.cc:38-56,110-125): h = (h ^ byte) * (2^88 + 315) mod 2^128.
 //
-// The hash is a serial chain over the bytes of one packet, so one lane owns one packet and
-// does everything for it: it streams the packet's bytes once (16-byte loads, two 64-byte
-// chunks in flight), hashes them and writes them to the output as they pass (a per-lane
-// dword writer that realigns with one 64-bit shift), then writes the tag.
+// The hash is a serial chain over the bytes of one packet, so one lane owns one packet's
+// chain, while the bytes move in wave tiles (tile_stream): a wave's 64 packets stream through
+// an 8 KB LDS tile in 128-byte windows.  Per window, 8 global_load_lds_dwordx4 bring 8
+// packets x 128 contiguous bytes each (chunk c of packet q at slot c ^ (q & 7), an XOR
+// swizzle so the lanes reading their own rows hit distinct banks); lane q hashes its packet's
+// valid bytes from LDS and writes each full 16-byte output line (realigned to the output's byte
+// phase, zeros past the source) back into the slot it consumed; then 8 coalesced non-temporal
+// global_store_dwordx4 in the same shape.  The two partial output lines at a packet's ends are
+// written byte by byte after the loop, batched over the wave.  Then the tag.
 //
-// The chain: h is kept as six 22-bit limbs in carry-save form.  h * 315 is six full-rate
-// 24-bit multiplies (v_mul_u32_u24; a limb stays below 2^24, its product below 2^32), each
-// limb keeps its low 22 bits and passes the rest up one limb, and h << 88 is two limb adds
-// (88 = 4 * 22): about 25 full-rate VALU operations per byte, with six independent lanes of
-// work, against seven quarter-rate 32-bit multiplies for a 64-bit-halves form.  The
-// low limb is always exact (nothing carries into it), so the byte XOR is exact too; the
-// limbs are normalised once, for the tag.  Bound: the VALU.
+// The chain: h mod 2^96 (the tag is its low 96 bits) is kept as five 22-bit limbs in
+// carry-save form.  h * 315 is five full-rate 24-bit multiplies (v_mul_u32_u24; limbs 0..3
+// stay below 2^24, their products below 2^32), each limb keeps its low 22 bits and passes the
+// rest up one limb, and h << 88 mod 2^96 is one add of the low byte's limb into limb 4
+// (88 = 4 * 22; r05 kept six limbs, mod 2^128).  The low limb is always exact (nothing
+// carries into it), so the byte XOR is exact too; the limbs are normalised once, for the
+// tag.  Bound: the VALU and the chain's latency.
 //
 // Grouped forms (the FEC group's view of its packets): every data and FEC packet of G groups
 // sealed in one launch, and the receiver's open that writes each data packet's plaintext
@@ -39,33 +44,33 @@ namespace {
 constexpr int kPPThreads = 256;   // one packet per lane
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// FNV-1a-128, six 22-bit limbs (limb j = bits 22j ..), carry-save: limbs 1..5 may exceed
-// 22 bits by the carry they received (< 2^24 always).
+// FNV-1a-128 modulo 2^96: the tag is the low 96 bits of the hash (quic_utils.cc:175-181,
+// null_encrypter.cc:23-43; the decrypter compares the same bits), and arithmetic mod 2^128
+// reduces to arithmetic mod 2^96, so bits 96..127 are never formed.  Five 22-bit limbs (limb j
+// = bits 22j ..), carry-save: limbs 1..3 may exceed 22 bits by the carry they received (< 2^24
+// always); limb 4 (bits 88..) is kept unmasked, only its low 8 bits count.  h * P =
+// h * 315 + (h << 88): mod 2^96 the shifted term is the low byte of h ^ byte added to limb 4.
 struct Fnv {
-    uint32_t l0, l1, l2, l3, l4, l5;
-    // kOffset = 144066263297769815596495629667062367629 (quic_utils.cc:116-118)
+    uint32_t l0, l1, l2, l3, l4;
+    // kOffset = 144066263297769815596495629667062367629 (quic_utils.cc:116-118), low 96 bits
     __device__ __forceinline__ void init() {
         l0 = 0x15c58du;
         l1 = 0x05d58au;
         l2 = 0x262b82u;
         l3 = 0x2ec050u;
         l4 = 0x272e07u;
-        l5 = 0x01b188u;
     }
     __device__ __forceinline__ void byte(uint32_t b) {
         constexpr uint32_t M = (1u << 22) - 1u;
         const uint32_t x0 = l0 ^ b;   // l0 < 2^22 is exact: the XOR is the reference's
         const uint32_t p0 = __umul24(x0, 315u), p1 = __umul24(l1, 315u);
         const uint32_t p2 = __umul24(l2, 315u), p3 = __umul24(l3, 315u);
-        const uint32_t p4 = __umul24(l4, 315u), p5 = __umul24(l5, 315u);
-        const uint32_t n4 = (p4 & M) + (p3 >> 22) + x0;   // + (h << 88), limbs 0, 1 -> 4, 5
-        const uint32_t n5 = (p5 & M) + (p4 >> 22) + l1;   // bits >= 128 fall off the top
+        const uint32_t p4 = __umul24(l4, 315u);   // low 24 bits of l4: its low 8 are exact
+        l4 = p4 + (p3 >> 22) + x0;                // + (h << 88) mod 2^96
         l1 = (p1 & M) + (p0 >> 22);
         l2 = (p2 & M) + (p1 >> 22);
         l3 = (p3 & M) + (p2 >> 22);
         l0 = p0 & M;
-        l4 = n4;
-        l5 = n5;
     }
     __device__ __forceinline__ void word(uint32_t w) {
         byte(w & 0xFFu);
@@ -76,20 +81,19 @@ struct Fnv {
     // the low 96 bits of h, little-endian dwords (SerializeUint128Short, quic_utils.cc:175-181)
     __device__ __forceinline__ void tag(uint32_t& t0, uint32_t& t1, uint32_t& t2) const {
         constexpr uint32_t M = (1u << 22) - 1u;
-        uint32_t c = 0, n[6];
-        const uint32_t l[6] = {l0, l1, l2, l3, l4, l5};
+        uint32_t c = 0, n[5];
+        const uint32_t l[5] = {l0, l1, l2, l3, l4};
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
+        for (int j = 0; j < 5; ++j) {
             const uint32_t v = l[j] + c;
             n[j] = v & M;
             c = v >> 22;
         }
         const uint64_t lo = (uint64_t)n[0] | ((uint64_t)n[1] << 22) | ((uint64_t)n[2] << 44);
-        const uint64_t hi = ((uint64_t)n[2] >> 20) | ((uint64_t)n[3] << 2) |
-                            ((uint64_t)n[4] << 24) | ((uint64_t)n[5] << 46);
+        const uint32_t hi = (n[2] >> 20) | (n[3] << 2) | (n[4] << 24);
         t0 = (uint32_t)lo;
         t1 = (uint32_t)(lo >> 32);
-        t2 = (uint32_t)hi;
+        t2 = hi;
     }
 };
 

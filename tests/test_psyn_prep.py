@@ -14,7 +14,8 @@ import pytest
 
 from quic_amd import synth
 
-PSYN = [(10, 10), (10, 15), (10, 20), (15, 15)]
+PSYN = [(10, 10), (10, 15), (10, 20), (15, 15), (5, 5)]
+CAUCHY_PSYN = [(10, 10), (10, 15), (10, 20), (15, 15)]   # m >= 7: column-scaled Cauchy
 
 
 def _gf(oracle):
@@ -38,7 +39,7 @@ def full_matrix(oracle, k, m):
     return np.concatenate([np.ones((1, k), np.uint8), oracle.cauchy_matrix(k, m)], axis=0)
 
 
-@pytest.mark.parametrize("k,m", PSYN)
+@pytest.mark.parametrize("k,m", CAUCHY_PSYN)
 def test_preset_matrix_is_scaled_cauchy(oracle, gf, k, m):
     mul, inv = gf
     C = full_matrix(oracle, k, m)
@@ -57,6 +58,37 @@ def test_preset_matrix_is_scaled_cauchy(oracle, gf, k, m):
             assert C[y][x] == mul[b[x], inv[b[x] ^ g[y]]]
     assert len(set(b.tolist())) == k and len(set(g.tolist())) == m
     assert not set(b.tolist()) & set(g.tolist())
+
+
+def _nonsingular(mul, inv, S):
+    """Gaussian elimination with pivoting over GF(256): is the square matrix S invertible?"""
+    S = S.copy()
+    r = S.shape[0]
+    for p in range(r):
+        nz = [i for i in range(p, r) if S[i][p]]
+        if not nz:
+            return False
+        S[[p, nz[0]]] = S[[nz[0], p]]
+        iv = int(inv[S[p][p]])
+        for i in range(p + 1, r):
+            if S[i][p]:
+                S[i] ^= mul[int(mul[S[i][p], iv]), S[p]]
+    return True
+
+
+def test_fec_5_5_matrix_every_square_submatrix_nonsingular(oracle, gf):
+    """FEC_5_5's matrix (the ones row and CAUCHY_MATRIX_5's rows, cauchy_256.cpp:428-442) is
+    not built from Cauchy nodes in the code, so gf_psyn's no-pivoting Gauss-Jordan is justified
+    exhaustively instead: every r x r submatrix (any r received parity rows, any r erased data
+    rows) is nonsingular, hence every leading minor of the prep's S is nonzero."""
+    import itertools
+    mul, inv = gf
+    k = m = 5
+    C = full_matrix(oracle, k, m)
+    for r in range(1, 6):
+        for ys in itertools.combinations(range(m), r):
+            for xs in itertools.combinations(range(k), r):
+                assert _nonsingular(mul, inv, C[np.ix_(ys, xs)]), (ys, xs)
 
 
 def bitsliced_apply(mul, c, block):
@@ -131,7 +163,8 @@ def test_model_matches_oracle(oracle, gf, k, m):
         rows = [x for x in range(k) if x not in lost] + [k + y for y in par]
         if g == 3:                                   # a repeated data row as an extra
             rows = list(range(k))
-            rows[5], rows[7] = 6, k + 2
+            a, b = (5, 7) if k >= 8 else (1, 3)
+            rows[a], rows[b] = a + 1, k + 2
         rows = np.array(rows)[rng.permutation(k)]
         sent = np.concatenate([data[g], p_or[g]])
         blocks = sent[rows].copy()

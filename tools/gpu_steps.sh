@@ -11,11 +11,14 @@
 #   quick:<W>[:<args>]    bench.py --workload W, no CPU baseline, no host leg, 10 steps
 #   preset:<k>,<m>        quick bench of a QuicR preset
 #   prof:<W>[:<args>]     rocprofv3 --kernel-trace --stats of a quick bench
+#   proflib:<name>,<W>[:<args>]  the same against quic_amd/libquic_fec_<name>.so
 #   abold:<W>[:<args>]    quick bench against quic_amd/libquic_fec_abold.so (an A/B build)
-#   libq:<name>,<W>[:<args>]  quick bench against quic_amd/libquic_fec_<name>.so
+#   libq:<name>,<W>[:<args>]  quick bench against quic_amd/libquic_fec_<name>.so (W = A..D or
+#                         P<k>_<m> for a QuicR preset)
 #   aboldp:<k>,<m>        the same for a QuicR preset
 #   pmc:<W>[:<args>]      tools/pmc.sh passes (FETCH/WRITE traffic, waves, issue mix)
 #   pmcold:<W>[:<args>]   the same against quic_amd/libquic_fec_abold.so
+#   pmclib:<name>,<W>[:<args>]  the same against quic_amd/libquic_fec_<name>.so
 # Extra args use '+' for spaces: quick:B:--opt+bsyn_depth=3.  GPU_STEPS_DRY=1 prints the steps.
 export TMPDIR=/tmp
 specs=()
@@ -42,10 +45,16 @@ for step in "$@"; do
     preset) specs+=("$tag::300::$quick --preset $W $extra") ;;
     aboldp) specs+=("$tag::300::QFEC_LIB_PATH=quic_amd/libquic_fec_abold.so $quick --preset $W $extra") ;;
     libq)   L="${W%%,*}"; WW="${W#*,}"
-            specs+=("$tag::300::QFEC_LIB_PATH=quic_amd/libquic_fec_$L.so $quick --workload $WW $extra") ;;
+            case "$WW" in P*_*) wl="--preset ${WW#P}"; wl="${wl/_/,}" ;; *) wl="--workload $WW" ;; esac
+            specs+=("$tag::300::QFEC_LIB_PATH=quic_amd/libquic_fec_$L.so $quick $wl $extra") ;;
     abold)  specs+=("$tag::300::QFEC_LIB_PATH=quic_amd/libquic_fec_abold.so $quick --workload $W $extra") ;;
     prof)   specs+=("$tag::300::rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run --output-format csv -- $quick --workload $W $extra") ;;
+    proflib) L="${W%%,*}"; WW="${W#*,}"
+            case "$WW" in P*_*) wl="--preset ${WW#P}"; wl="${wl/_/,}" ;; *) wl="--workload $WW" ;; esac
+            specs+=("$tag::300::QFEC_LIB_PATH=quic_amd/libquic_fec_$L.so rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run --output-format csv -- $quick $wl $extra") ;;
     pmc)    specs+=("$tag::600::bash tools/pmc.sh $W $tag $extra") ;;
+    pmclib) L="${W%%,*}"; WW="${W#*,}"
+            specs+=("$tag::600::QFEC_LIB_PATH=quic_amd/libquic_fec_$L.so bash tools/pmc.sh $WW $tag $extra") ;;
     pmcold) specs+=("$tag::600::QFEC_LIB_PATH=quic_amd/libquic_fec_abold.so bash tools/pmc.sh $W $tag $extra") ;;
     *) echo "unknown step: $step"; exit 2 ;;
   esac
