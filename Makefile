@@ -20,11 +20,11 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
 DCOLK := e63 e83 d62 d82
 # preset syndrome-decode instantiations, one object per code (gf_psyn.h)
 PSYNK := 1010 1015 1020 1515 55
-SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_stream.hip $(CSRC)/gf_bsyn.hip $(CSRC)/gf_rsyn.hip $(CSRC)/gf_psyn.hip $(PSYNK:%=$(CSRC)/gf_psyn_%.hip) $(CSRC)/gf_dcol.hip $(DCOLK:%=$(CSRC)/gf_dcol_%.hip) $(CSRC)/pp_null.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp $(CSRC)/fec_wire.cpp
+SRCS := $(CSRC)/fec_kernels.hip $(CSRC)/xor_dma.hip $(CSRC)/gf_stream.hip $(CSRC)/gf_bsyn.hip $(CSRC)/gf_psyn.hip $(PSYNK:%=$(CSRC)/gf_psyn_%.hip) $(CSRC)/gf_dcol.hip $(DCOLK:%=$(CSRC)/gf_dcol_%.hip) $(CSRC)/pp_null.hip $(CSRC)/fec_api.cpp $(CSRC)/fec_group.cpp $(CSRC)/fec_wire.cpp
 # the headers every object depends on; the rest (include/*.h, pp_null.h, ...) are tracked per
 # object by -MMD below, so a public-header edit rebuilds only the host files that include it
 HDRS := $(CSRC)/fec_kernels.h $(CSRC)/gf256.h $(CSRC)/gf_bitslice.h
-OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/xor_dma.o $(ROOT)build/gf_stream.o $(ROOT)build/gf_bsyn.o $(ROOT)build/gf_rsyn.o $(ROOT)build/gf_psyn.o $(PSYNK:%=$(ROOT)build/gf_psyn_%.o) $(ROOT)build/gf_dcol.o $(DCOLK:%=$(ROOT)build/gf_dcol_%.o) $(ROOT)build/pp_null.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o $(ROOT)build/fec_wire.o
+OBJS := $(ROOT)build/fec_kernels.o $(ROOT)build/xor_dma.o $(ROOT)build/gf_stream.o $(ROOT)build/gf_bsyn.o $(ROOT)build/gf_psyn.o $(PSYNK:%=$(ROOT)build/gf_psyn_%.o) $(ROOT)build/gf_dcol.o $(DCOLK:%=$(ROOT)build/gf_dcol_%.o) $(ROOT)build/pp_null.o $(ROOT)build/fec_api.o $(ROOT)build/fec_group.o $(ROOT)build/fec_wire.o
 
 # Build guard (tools/check_stubs.py): every kernel stub a host pass registers has device code
 # in the same object.  Run after each HIP compile (the object is deleted on a mismatch) and on
@@ -90,11 +90,6 @@ $(ROOT)build/gf_stream.o: $(CSRC)/gf_stream.hip $(CSRC)/gf_winjump.h $(HDRS) $(G
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }
 
 $(ROOT)build/gf_bsyn.o: $(CSRC)/gf_bsyn.hip $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
-	@mkdir -p $(ROOT)build
-	$(HIPCC) $(HIPFLAGS) $(SAVE_ASM) -c $< -o $@
-	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }
-
-$(ROOT)build/gf_rsyn.o: $(CSRC)/gf_rsyn.hip $(CSRC)/gf_winjump.h $(HDRS) $(GEN) $(WJGEN)
 	@mkdir -p $(ROOT)build
 	$(HIPCC) $(HIPFLAGS) $(SAVE_ASM) -c $< -o $@
 	@$(STUBCHECK) $@ || { rm -f $@; exit 1; }

@@ -146,7 +146,6 @@ struct HostBuf {
 // One decode workspace: the prep's per-group tables and the in-place scratch.
 struct Workspace {
     DevBuf dcoef, dslots, dnout, dscratch;
-    DevBuf dlist;   // (32, 4) ring decode: [0] = count, then the slow groups' indices
     // graph workspace: a buffer outgrown by a later capture is kept (not freed) until the
     // context is destroyed, since the graphs captured before still name it
     bool keep = false;
@@ -293,29 +292,18 @@ int decode_workspace(Workspace& W, int k, int rmax, int rc, long long groups) {
     QF_HIP(W.ensure(W.dcoef, (size_t)groups * per));
     QF_HIP(W.ensure(W.dslots, (size_t)groups * rmax));
     QF_HIP(W.ensure(W.dnout, (size_t)groups * sizeof(int32_t)));
-    QF_HIP(W.ensure(W.dlist, (size_t)(groups + 1) * sizeof(int32_t)));
     return 0;
 }
 
-// The (32, 4) x 1352 B syndrome decode (configs B / C): prep, then gf_rsyn for the groups whose
-// slots hold rows near their index (packet-number order and the like) and gf_bsyn for the
-// others, listed by the prep (bsyn_ring = 0: gf_bsyn for every group).
-int bsyn_decode(qfec_ctx* c, Workspace& W, const uint8_t* d_blocks, const uint8_t* d_rows_in,
+// The (32, 4) x 1352 B syndrome decode (configs B / C): prep, then gf_bsyn.
+int bsyn_decode(qfec_ctx* c, const uint8_t* d_blocks, const uint8_t* d_rows_in,
                 uint8_t* d_rows_out, uint8_t* d_out, uint8_t* d_rec_rows, int32_t* d_status,
                 const uint8_t* cenc, qfec::DecodeWork w, int k, int m, int bb, int rmax,
                 long long G, long long out_gstride, const uint8_t* slots, hipStream_t st) {
-    int32_t* slow = nullptr;
-    if (c->tune.bsyn_ring) {
-        slow = (int32_t*)W.dlist.p;
-        QF_HIP(hipMemsetAsync(slow, 0, sizeof(int32_t), st));
-    }
     QF_HIP(qfec::launch_decode_prep_bsyn(d_rows_in, d_rows_out, d_status, cenc, w.coef, w.slots,
-                                         w.nout, d_rec_rows, k, m, bb, rmax, G, st, slow));
-    if (slow)
-        QF_HIP(qfec::launch_gf_rsyn(d_blocks, d_out, w.coef, slots, w.nout, k, m, bb, G, rmax,
-                                    out_gstride, st, c->tune));
+                                         w.nout, d_rec_rows, k, m, bb, rmax, G, st));
     QF_HIP(qfec::launch_gf_bsyn(d_blocks, d_out, w.coef, cenc, slots, w.nout, k, m, bb, G, rmax,
-                                out_gstride, st, c->tune, slow));
+                                out_gstride, st, c->tune));
     return 0;
 }
 
@@ -407,7 +395,7 @@ int decode_body(qfec_ctx* c, int k, int m, int bb, long long G, const uint8_t* d
     if (qfec::gf_bsyn_supported(k, m, bb, rmax, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
         // compiled (32, 4) code: syndromes of every parity row, then the r x r solve (a
         // group's stores follow all of its reads: in place needs no scratch)
-        return bsyn_decode(c, W, d_blocks, d_rows_in, d_rows_out, d_out, nullptr, d_status, cenc,
+        return bsyn_decode(c, d_blocks, d_rows_in, d_rows_out, d_out, nullptr, d_status, cenc,
                            w, k, m, bb, rmax, G, (long long)k * bb, w.slots, st);
     }
     QF_HIP(qfec::launch_decode_prep(d_rows_in, d_rows_out, d_status, cenc, w, k, m, bb, rc, rmax,
@@ -504,7 +492,7 @@ int decode_recovered_body(qfec_ctx* c, int k, int m, int bb, long long G,
         return 0;
     }
     if (qfec::gf_bsyn_supported(k, m, bb, rmax, c->tune) && ((uintptr_t)d_blocks & 15) == 0) {
-        return bsyn_decode(c, W, d_blocks, d_rows_in, nullptr, d_rec, d_rec_rows, d_status, cenc,
+        return bsyn_decode(c, d_blocks, d_rows_in, nullptr, d_rec, d_rec_rows, d_status, cenc,
                            w, k, m, bb, rmax, G, (long long)rmax * bb, nullptr, st);
     }
     QF_HIP(qfec::launch_decode_prep(d_rows_in, nullptr, d_status, cenc, w, k, m, bb, rc, rmax, G,
@@ -728,7 +716,6 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"dcol", &t.dcol, 0, 1},               {"dcol_grid", &t.dcol_grid, 0, 1 << 20},
         {"dcol_depth", &t.dcol_depth, 6, 8},
         {"bsyn", &t.bsyn, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
-        {"bsyn_ring", &t.bsyn_ring, 0, 1},
         {"psyn", &t.psyn, 0, 1},
         {"pd", &t.pd, 1, 3},                   {"flat", &t.flat, 0, 1},
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
@@ -756,7 +743,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"ring_wide", t.ring_wide}, {"psyn_wide", t.psyn_wide},
         {"dcol", t.dcol},
         {"dcol_grid", t.dcol_grid}, {"dcol_depth", t.dcol_depth},
-        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"bsyn_ring", t.bsyn_ring}, {"psyn", t.psyn},
+        {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"psyn", t.psyn},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb}, {"host_min_groups", t.host_min_groups},
     };

@@ -35,9 +35,6 @@ struct Tune {
     int bsyn = 1;             // (32, 4) x 1352 B decode: compiled syndrome kernel gf_bsyn
                               //   (0: the run-time gf_stream decode)
     int bsyn_depth = 3;       // gf_bsyn: blocks in flight per wave (3, 5, 7; 3: 5 waves/SIMD)
-    int bsyn_ring = 0;        // (32, 4) decode: gf_rsyn (static ring stream in slot order) for the
-                              //   groups whose slots hold rows near their index, gf_bsyn for
-                              //   the rest (0: gf_bsyn for every group)
     int psyn = 1;             // QuicR presets with m >= 7 and (5, 5) at 1352 B: compiled syndrome decode
                               //   gf_psyn (0: the run-time gf_stream decode)
     int dcol = 1;             // (128, 16) x 9008 B: gf_dcol (one wave per column tile, all 16
@@ -123,12 +120,7 @@ constexpr int kMask = 64;    // u32[2] bit x: data row x is in the ascending par
 constexpr int kY = 72;       // u8[4]  parity row y_i of recovery block i
 constexpr int kSinv = 76;    // u8[4][4] Sinv[j][i]: recovered j = sum_i Sinv[j][i] T_{y_i}
 constexpr int kERow = 92;    // u8[64] row tag of extra e (255: no-op, unchanged group)
-constexpr int kRows = 156;   // u8[64] row tag of slot i (gf_rsyn)
-constexpr int kFast = 220;   // u32    1: gf_rsyn decodes this group in its slot-order ring
-                             //        stream (every data slot i holds a row in [i, i + 4]);
-                             //        0: nothing to do, or the group is on the slow list
-constexpr int kBytes = 224;
-constexpr int kRsynE = 4;    // largest row - slot offset gf_rsyn compiles
+constexpr int kBytes = 156;
 }  // namespace bsyn
 
 // Preset syndrome table (decode_prep_psyn, read by gf_psyn), one per group at
@@ -235,24 +227,15 @@ hipError_t launch_gf_dcol_syndrome(const uint8_t* in, uint8_t* out, const uint8_
 
 // Syndrome decode of the compiled (32, 4) x 1352-byte code (gf_bsyn.hip): prep (bsyn::
 // table, one lane per group) and the block pass + r x r solve.
-// With `slow` (ring mode, gf_rsyn): the prep marks each group gf_rsyn can decode in its
-// slot-order stream (bsyn::kFast) and appends every other changed group's index to slow[1..]
-// (slow[0] = their count, zeroed by the caller first); gf_bsyn then decodes only the listed
-// groups (slow != null), gf_rsyn the marked ones.
 bool gf_bsyn_supported(int k, int m, int bb, int rmax, const Tune& t);
 hipError_t launch_decode_prep_bsyn(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
                                    const uint8_t* cenc, uint8_t* tab, uint8_t* slots,
                                    int32_t* nout, uint8_t* rec_rows, int k, int m, int bb,
-                                   int rmax, long long groups, hipStream_t st,
-                                   int32_t* slow = nullptr);
+                                   int rmax, long long groups, hipStream_t st);
 hipError_t launch_gf_bsyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
                           const uint8_t* cenc, const uint8_t* slots, const int32_t* nout, int k,
                           int m, int bb, long long groups, int rmax, long long out_gstride,
-                          hipStream_t st, const Tune& t, const int32_t* slow = nullptr);
-hipError_t launch_gf_rsyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
-                          const uint8_t* slots, const int32_t* nout, int k, int m, int bb,
-                          long long groups, int rmax, long long out_gstride, hipStream_t st,
-                          const Tune& t);
+                          hipStream_t st, const Tune& t);
 
 // Syndrome decode of the compiled QuicR preset codes with m >= 7 and (5, 5) at 1352-byte blocks
 // (gf_psyn.hip): prep (psyn:: table, 16 lanes per group) and the block pass + in-place

@@ -97,13 +97,11 @@ constexpr int kBsynRC = 4;      // recovered blocks per group (rmax <= 4)
 
 // KC, MC: the compiled code (k, m); S: sub-row bytes; D: blocks in flight per wave.
 // NTS: the recovered blocks are stored non-temporal
-// slow != null: only the groups slow[1 .. slow[0]] (gf_rsyn decodes the others)
 template <int KC, int MC, int S, int D, bool NTS = false>
 __global__ __launch_bounds__(kBsynWaves * 64) void gf_bsyn_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ tab,
     const uint8_t* __restrict__ cenc, const uint8_t* __restrict__ slots,
-    const int32_t* __restrict__ nout, long long groups, int rmax, long long out_gstride,
-    const int32_t* __restrict__ slow) {
+    const int32_t* __restrict__ nout, long long groups, int rmax, long long out_gstride) {
     using SH = BsynShape<S>;
     constexpr int BB = SH::BB, NW = SH::NW, NWF = SH::NWF, SPR = SH::SPR;
     constexpr int BUFB = SH::BUFB, NPC = SH::NPC, P1L = SH::P1L;
@@ -121,23 +119,19 @@ __global__ __launch_bounds__(kBsynWaves * 64) void gf_bsyn_kernel(
     uint8_t* ring = smem + (size_t)w * NB * BUFB;
     const long long W = (long long)gridDim.x * kBsynWaves;
     const long long g0 = (long long)blockIdx.x * kBsynWaves + w;
-    if (slow) groups = (long long)bsyn_cload_u32((const uint8_t*)slow, 0);
     if (g0 >= groups) return;
     const int cnt = __builtin_amdgcn_readfirstlane((int)((groups - 1 - g0) / W + 1));
     const int c = lane < NW ? lane : NW - 1;  // idle lanes shadow the last word
-    // the group of list entry li (every group when there is no list)
-    auto gid = [&](long long li) __attribute__((always_inline)) -> long long {
-        return slow ? (long long)bsyn_cload_u32((const uint8_t*)slow, (int)(4 * (li + 1))) : li;
-    };
 
     // ---- DMA side: stream block b = position iss_x of group g0 + i * W, the slot the table
     // names there, into ring buffer iss_buf; bit iss_buf of `skew` = its 8-byte skew.  Past
     // the stream's end the last block is re-read (every step issues and waits the same way).
     int iss_buf = 0, iss_x = 0;
     int iss_left = cnt * KC;
-    long long iss_li = g0;
-    const uint8_t* iss_g = in + gid(g0) * (long long)(KC * BB);
-    const uint8_t* iss_t = tab + gid(g0) * (long long)bsyn::kBytes;
+    const uint8_t* iss_g = in + g0 * (long long)(KC * BB);
+    const uint8_t* iss_t = tab + g0 * (long long)bsyn::kBytes;
+    const long long gstride = W * (long long)(KC * BB);
+    const long long tstride = W * (long long)bsyn::kBytes;
     uint32_t perm_w = 0, skew = 0;
     auto issue_next = [&]() __attribute__((always_inline)) {
         if ((iss_x & 3) == 0) perm_w = bsyn_cload_u32(iss_t, bsyn::kPerm + iss_x);
@@ -153,10 +147,8 @@ __global__ __launch_bounds__(kBsynWaves * 64) void gf_bsyn_kernel(
         if (++iss_buf == NB) iss_buf = 0;
         if (--iss_left > 0 && ++iss_x == KC) {
             iss_x = 0;
-            iss_li += W;
-            const long long gn = gid(iss_li);
-            iss_g = in + gn * (long long)(KC * BB);
-            iss_t = tab + gn * (long long)bsyn::kBytes;
+            iss_g += gstride;
+            iss_t += tstride;
         }
     };
     // column word c of the 8 sub-rows of stream block bi: aligned dwords (the buffer start
@@ -186,7 +178,7 @@ __global__ __launch_bounds__(kBsynWaves * 64) void gf_bsyn_kernel(
     int prev_n = -1;  // recovered blocks the previous group stored (-1: no previous group)
 #pragma unroll 1
     for (int i = 0; i < cnt; ++i) {
-        const long long g = gid(g0 + (long long)i * W);
+        const long long g = g0 + (long long)i * W;
         const uint8_t* tb = tab + g * (long long)bsyn::kBytes;
         const uint32_t mlo = bsyn_cload_u32(tb, bsyn::kMask), mhi = bsyn_cload_u32(tb, bsyn::kMask + 4);
         const uint32_t ymap = bsyn_cload_u32(tb, bsyn::kY);
@@ -354,7 +346,7 @@ __global__ __launch_bounds__(256) void decode_prep_bsyn_kernel(
     const uint8_t* __restrict__ rows_in, uint8_t* rows_out, int32_t* __restrict__ status,
     const uint8_t* __restrict__ cenc, uint8_t* __restrict__ tab, uint8_t* __restrict__ slots,
     int32_t* __restrict__ nout, uint8_t* __restrict__ rec_rows, long long groups, int k, int m,
-    int bb, int rmax, int32_t* __restrict__ slow) {
+    int bb, int rmax) {
     __shared__ uint8_t gexp[512];
     __shared__ uint8_t glog[256];
     extern __shared__ __attribute__((aligned(16))) uint8_t lsm[];
@@ -499,17 +491,6 @@ __global__ __launch_bounds__(256) void decode_prep_bsyn_kernel(
         *(uint32_t*)(T + bsyn::kMask) = 0;
         *(uint32_t*)(T + bsyn::kMask + 4) = 0;
     }
-    // gf_rsyn (ring mode): the slots' row tags, and whether its slot-order stream takes this
-    // group (every data slot i holds a row in [i, i + kRsynE]); a changed group it does not
-    // take goes on gf_bsyn's list
-    bool fast = n > 0;
-    for (int i = 0; i < k; ++i) {
-        const int r = rg[i];
-        T[bsyn::kRows + i] = (uint8_t)r;
-        if (r < k && (r < i || r > i + bsyn::kRsynE)) fast = false;
-    }
-    *(uint32_t*)(T + bsyn::kFast) = (slow && fast) ? 1u : 0u;
-    if (slow && live && n > 0 && !fast) slow[1 + atomicAdd(slow, 1)] = (int32_t)g;
     if (live) {
         const uint8_t* rgg = rows_in + g * k;
         uint8_t* ro = rows_out ? rows_out + g * k : nullptr;
@@ -544,7 +525,7 @@ bool gf_bsyn_supported(int k, int m, int bb, int rmax, const Tune& t) {
 hipError_t launch_decode_prep_bsyn(const uint8_t* rows_in, uint8_t* rows_out, int32_t* status,
                                    const uint8_t* cenc, uint8_t* tab, uint8_t* slots,
                                    int32_t* nout, uint8_t* rec_rows, int k, int m, int bb,
-                                   int rmax, long long groups, hipStream_t st, int32_t* slow) {
+                                   int rmax, long long groups, hipStream_t st) {
     if (groups <= 0) return hipSuccess;
     if (k > 64 || k % 4 != 0 || rmax > 4 || (long long)m * k > 4096 ||
         ((((uintptr_t)tab) | (uintptr_t)rows_in) & 3))
@@ -554,14 +535,14 @@ hipError_t launch_decode_prep_bsyn(const uint8_t* rows_in, uint8_t* rows_out, in
                        256 * (size_t)bsyn::kBytes;
     note_kernel("decode_prep_bsyn_kernel");
     qlaunch((decode_prep_bsyn_kernel), dim3(nb), dim3(256), lds, st, rows_in, rows_out, status,
-            cenc, tab, slots, nout, rec_rows, groups, k, m, bb, rmax, slow);
+            cenc, tab, slots, nout, rec_rows, groups, k, m, bb, rmax);
     return hipGetLastError();
 }
 
 hipError_t launch_gf_bsyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
                           const uint8_t* cenc, const uint8_t* slots, const int32_t* nout, int k,
                           int m, int bb, long long groups, int rmax, long long out_gstride,
-                          hipStream_t st, const Tune& t, const int32_t* slow) {
+                          hipStream_t st, const Tune& t) {
     if (groups <= 0) return hipSuccess;
     if (!gf_bsyn_supported(k, m, bb, rmax, t)) return hipErrorInvalidValue;
     if ((((uintptr_t)in) & 15) || ((((uintptr_t)tab) | (uintptr_t)cenc | (uintptr_t)slots) & 3))
@@ -582,7 +563,7 @@ hipError_t launch_gf_bsyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
     // recovered blocks stored non-temporal (B decode 0.655 -> 0.631 ms)
 #define QB_GO(DV)                                                                             \
     qlaunch((gf_bsyn_kernel<32, 4, kBsynS, DV, true>), dim3(grid), dim3(kBsynWaves * 64), lds, \
-            st, in, out, tab, cenc, slots, nout, groups, rmax, out_gstride, slow)
+            st, in, out, tab, cenc, slots, nout, groups, rmax, out_gstride)
     switch (D) {
         case 3: QB_GO(3); break;
         case 5: QB_GO(5); break;

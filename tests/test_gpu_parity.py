@@ -459,7 +459,7 @@ OPTION_SETS = [
     {"dma": 0}, {"stream": 0}, {"stream": 0, "pd": 1}, {"stream": 0, "pd": 3},
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
     {"stream_ring": 36}, {"host_chunk_mb": 1, "host_min_groups": 1}, {"const_enc": 0},
-    {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 5}, {"bsyn_depth": 7}, {"bsyn_ring": 0},
+    {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 5}, {"bsyn_depth": 7},
     {"dcol": 0}, {"dcol_depth": 8},
     {"psyn": 0},
 ]
@@ -468,7 +468,8 @@ OPTION_SETS = [
 # measured-and-rejected variants and timing probes are not options of the product ABI
 # (DESIGN.md section 3.7): qfec_ctx_set_option refuses them with -2
 REMOVED_OPTIONS = ["psyn_ablate", "enc_split", "wide_st", "stream_rc16", "dcol_rows", "dcol_cache",
-                   "psyn_jump", "psyn_pf", "psyn_depth", "ring_nt", "dec_nt", "stream_jump", "pp_hash"]
+                   "psyn_jump", "psyn_pf", "psyn_depth", "ring_nt", "dec_nt", "stream_jump", "pp_hash",
+                   "bsyn_ring"]
 
 
 @pytest.mark.parametrize("name", REMOVED_OPTIONS)
@@ -984,23 +985,19 @@ def test_graph_replay_then_eager_other_stream():
 
 
 # ------------------------------------------------- gf_bsyn (compiled (32, 4) decode, B/C)
-@pytest.mark.parametrize("ring", [1, 0])
 @pytest.mark.parametrize("depth", [3, 5, 7])
 @pytest.mark.parametrize("grid", [1, 2, 0])
-def test_bsyn_decode_patterns(tuned_engine, oracle, depth, grid, ring):
+def test_bsyn_decode_patterns(tuned_engine, oracle, depth, grid):
     """Configs B/C's decode (syndromes of every parity row with the compiled (32, 4) code, then
     the r x r solve, gf_bsyn_kernel) on hand-built receive sets: no loss, 1-4 losses with
     first / scattered / last parity rows, shuffled arrival (blocks streamed from any slot,
     odd slots 8 bytes off a 16-byte boundary), a repeated data row (an extra with run-time
     coefficients), malformed sets (status -3, group unchanged); the grid capped so a wave
     streams many groups back to back (the next group's blocks are prefetched across the
-    previous group's stores).  ring = 1 (default): the in-order groups (every data slot's row
-    within 4 of its index) go to gf_rsyn's slot-order ring stream and the shuffled ones to
-    gf_bsyn's list; ring = 0: gf_bsyn for every group."""
+    previous group's stores)."""
     engine = tuned_engine
     engine.set_option("stream_grid", grid)
     engine.set_option("bsyn_depth", depth)
-    engine.set_option("bsyn_ring", ring)
     k, m, bb = 32, 4, 1352
     rng = np.random.default_rng(300 + depth + grid)
     G = 24
@@ -1042,7 +1039,6 @@ def test_bsyn_decode_patterns(tuned_engine, oracle, depth, grid, ring):
     s_or = check_decodes(engine, oracle, k, m, bb, recv[ok], rows[ok],
                          "gf_bsyn_kernel<decode,k32m4>")
     assert (s_or == 0).all()
-    assert ("gf_rsyn_kernel<decode,k32m4>" in fec.last_kernels()) == bool(ring)
     b, rr, st = gpu_decode(engine, k, m, bb, recv[~ok], rows[~ok], inplace=True)
     assert st.tolist() == [-3, -3]
     np.testing.assert_array_equal(rr, rows[~ok])

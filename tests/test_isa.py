@@ -1,7 +1,7 @@
 """ISA guard for the counted-vmcnt kernels (CPU only: hipcc cross-compiles gfx950).
 
 gf_stream_kernel / gf_ring_kernel (quic_amd/csrc/gf_stream.hip), gf_bsyn_kernel (gf_bsyn.hip)
-gf_rsyn_kernel (gf_rsyn.hip), gf_psyn_kernel (gf_psyn.hip) and gf_dcol_kernel (gf_dcol.hip) keep their own count of the VMEM instructions they issued and wait with `s_waitcnt vmcnt(N)` for
+gf_psyn_kernel (gf_psyn.hip) and gf_dcol_kernel (gf_dcol.hip) keep their own count of the VMEM instructions they issued and wait with `s_waitcnt vmcnt(N)` for
 exactly the pieces a block needs.  That is only sound if the compiler emits no VMEM
 instruction outside the count (a global_load of a uniform byte, a register spill, say) and
 inserts no vmcnt wait of its own (which would drain the pipeline).  This test compiles the
@@ -23,7 +23,7 @@ DCOL = ["gf_dcol_e63", "gf_dcol_e83", "gf_dcol_d62", "gf_dcol_d82"]
 PSYN = ["gf_psyn_1010", "gf_psyn_1015", "gf_psyn_1020", "gf_psyn_1515", "gf_psyn_55"]
 
 
-@pytest.fixture(scope="module", params=["gf_stream", "gf_bsyn", "gf_rsyn"] + PSYN + DCOL)
+@pytest.fixture(scope="module", params=["gf_stream", "gf_bsyn"] + PSYN + DCOL)
 def stream_isa(tmp_path_factory, request):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
@@ -63,7 +63,7 @@ def stream_isa(tmp_path_factory, request):
     for m in re.finditer(r"^(_ZN4qfec(?:12_GLOBAL__N_1)?\d+gf_\w+?_kernel\w+):", text, re.M):   # every kernel
         end = text.index(".Lfunc_end", m.end())
         bodies[m.group(1)] = text[m.end():end]
-    assert len(bodies) >= (1 if name in DCOL + PSYN + ["gf_rsyn"] else 2), "expected the kernel instantiations"
+    assert len(bodies) >= (1 if name in DCOL + PSYN else 2), "expected the kernel instantiations"
     assert not re.search(r"\.private_segment_fixed_size:\s+[1-9]", text), "register spills"
     return bodies
 
