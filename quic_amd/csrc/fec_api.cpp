@@ -713,6 +713,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"stream_ring", &t.stream_ring, 4, 36}, {"stream_grid", &t.stream_grid, 0, 1 << 20},
         {"const_enc", &t.const_enc, 0, 1},     {"stream_static", &t.stream_static, 0, 1},
         {"ring_wide", &t.ring_wide, 0, 1}, {"psyn_wide", &t.psyn_wide, 0, 2},
+        {"ring_split", &t.ring_split, 0, 1},
         {"dcol", &t.dcol, 0, 1},               {"dcol_grid", &t.dcol_grid, 0, 1 << 20},
         {"dcol_depth", &t.dcol_depth, 6, 8},
         {"bsyn", &t.bsyn, 0, 1},               {"bsyn_depth", &t.bsyn_depth, 3, 7},
@@ -740,7 +741,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
     const std::pair<const char*, int> opts[] = {
         {"cus", t.cus}, {"xor_slots", t.xor_slots}, {"xor_waves", t.xor_waves}, {"dma", t.dma},
         {"stream", t.stream}, {"stream_ring", t.stream_ring}, {"stream_grid", t.stream_grid},
-        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"ring_wide", t.ring_wide}, {"psyn_wide", t.psyn_wide},
+        {"const_enc", t.const_enc}, {"stream_static", t.stream_static}, {"ring_wide", t.ring_wide}, {"psyn_wide", t.psyn_wide}, {"ring_split", t.ring_split},
         {"dcol", t.dcol},
         {"dcol_grid", t.dcol_grid}, {"dcol_depth", t.dcol_depth},
         {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"psyn", t.psyn},

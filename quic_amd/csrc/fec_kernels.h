@@ -26,6 +26,7 @@ struct Tune {
     int stream_grid = 0;      // gf_stream: grid cap in workgroups (0: CUs x per-CU fit)
     int stream_static = 1;    // gf_ring: compile-time ring schedule (B/C and preset encodes)
     int ring_wide = 1;        // gf_ring preset encodes: LDS-staged 8-byte parity stores
+    int ring_split = 1;       // gf_ring (10, 20) encode: two units of 10 parity rows per group
     int psyn_wide = 1;        // gf_psyn wide recovered-block stores: 1 (10, 10), 2 all
     int const_enc = 1;        // encode kernels specialised for fixed (k, m) where compiled
     int pd = 2;               // gf_apply: register pipeline depth (1..3)

@@ -62,10 +62,11 @@ __device__ __forceinline__ void stream_wait_dyn(int n) {
 // 16 bytes per lane from buffer rs at voff into LDS at lds + 16 * lane (nt); offsets past
 // the buffer's range load zeros.  (Device only: in a lambda the builtin would void the
 // kernel's host stub.)
+template <int AUX = 2>
 __device__ __forceinline__ void stream_dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds,
                                              uint32_t voff) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, QS_LPTR(lds), 16, voff, 0, 0, 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, QS_LPTR(lds), 16, voff, 0, 0, AUX);
 #else
     (void)rs, (void)lds, (void)voff;
 #endif
@@ -487,7 +488,12 @@ struct RingShape {
 // A group whose size is 8 mod 16 is streamed as GBS = GB + 8 bytes from the 16-byte boundary
 // at or below its start; the loads then go through a buffer resource bounded by the end of
 // the input (the last group's stream may end 8 bytes past it: those lanes read zeros).
-template <int K, int S, int RC, bool DECODE, int MC, bool NT, int SK, bool WIDE>
+// NCH > 1 (encode): a group's MC parity rows are NCH chunks of RC rows, one unit each; unit
+// u = NCH * g + ch, and a wave's units u0, u0 + W, ... (W a multiple of NCH) all have chunk
+// Y0 / RC = u0 % NCH, so the chunk's rows are compile-time; the NCH units of a group run on
+// neighbouring waves, whose reads of the group meet in L2.
+template <int K, int S, int RC, bool DECODE, int MC, bool NT, int SK, bool WIDE, int NCH = 1,
+          int Y0 = 0>
 __device__ __forceinline__ void gf_ring_run(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
@@ -506,7 +512,8 @@ __device__ __forceinline__ void gf_ring_run(
     constexpr int SAUX = (DECODE || !NT) ? 0 : 2;         // encode's parity stream: nt
     constexpr int FM1 = SH::pf(K - 1) + R - 1 - NP;       // next-group pieces issued early
     static_assert(!DECODE || MC == 0, "decode coefficients are per group");
-    static_assert(DECODE || MC == RC, "encode: one output per register set");
+    static_assert(DECODE || MC == RC * NCH, "encode: one output per register set");
+    static_assert(NCH == 1 || (!DECODE && Y0 % RC == 0 && Y0 < MC), "chunked encode");
     static_assert(FM1 >= SH::pl(0), "block 0 of the next group is prefetched in full");
     static_assert(SH::pf(K - 1) + R - 1 < 2 * NP, "the frontier stays within the next group");
     const int lane = threadIdx.x & 63;
@@ -515,8 +522,8 @@ __device__ __forceinline__ void gf_ring_run(
     const uint32_t stage =   // (WIDE) this wave's staging buffer (LDS address), after the rings
         (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(
             smem + (size_t)kRingWaves * RB + (size_t)w * kStreamStage);
-    const long long W = (long long)gridDim.x * kRingWaves;
-    const long long g0 = (long long)blockIdx.x * kRingWaves + w;
+    const long long W = (long long)gridDim.x * kRingWaves / NCH;   // group stride of the wave
+    const long long g0 = ((long long)blockIdx.x * kRingWaves + w) / NCH;
     if (g0 >= groups) return;
     const long long cnt =   // wave-uniform, kept in SGPRs (the division runs on the VALU)
         __builtin_amdgcn_readfirstlane((int)((groups - 1 - g0) / W + 1));      // groups of this wave
@@ -533,17 +540,20 @@ __device__ __forceinline__ void gf_ring_run(
     // and the lane offsets are two loop-invariant VGPRs instead of one per piece)
     const uint32_t v16 = 16u * (uint32_t)lane;
     const uint32_t vlast = min(16u * (uint32_t)lane, (uint32_t)(GBS - 16 - (NP - 1) * 1024));
+    // non-temporal loads, but default policy when a group's chunks are read by NCH waves
+    // (the sibling's reads then hit the lines in L2)
+    constexpr int LAUX = NCH > 1 ? 0 : 2;
     auto dma = [&](const uint8_t* src, int p, int slot) __attribute__((always_inline)) {
         if constexpr (SKEW) {
             const uint8_t* b = src + p * 1024;
             const long long left = in_end - b;
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)b, 0, (unsigned)(left < 1024 ? left : 1024), 0x00020000);
-            stream_dma16(rs, ring + slot * 1024, p == NP - 1 ? vlast : v16);
+            stream_dma16<LAUX>(rs, ring + slot * 1024, p == NP - 1 ? vlast : v16);
         } else {
             const int off = min(p * 1024 + lane * 16, GBS - 16);
             __builtin_amdgcn_global_load_lds(QS_GPTR(src + off), QS_LPTR(ring + slot * 1024), 16,
-                                             0, 2);
+                                             0, LAUX);
         }
     };
 
@@ -657,7 +667,7 @@ __device__ __forceinline__ void gf_ring_run(
                 win_build(v.W8, win);
                 static_for<RC>([&](auto jc) __attribute__((always_inline)) {
                     constexpr int j = decltype(jc)::value;
-                    win_apply<cauchy_coef(MC, j, x)>(acc[j], win);
+                    win_apply<cauchy_coef(MC, Y0 + j, x)>(acc[j], win);
                 });
             } else {
                 uint32_t cwv[NCW];
@@ -739,7 +749,7 @@ __device__ __forceinline__ void gf_ring_run(
             const uint32_t ra = stage + 8u * (uint32_t)lane;
 #pragma unroll
             for (int j = 0; j < RC; ++j) {
-                uint8_t* dst = out + g * out_gstride + (long long)j * BB;
+                uint8_t* dst = out + g * out_gstride + (long long)(Y0 + j) * BB;
                 const __amdgpu_buffer_rsrc_t rs =
                     __builtin_amdgcn_make_buffer_rsrc(dst, 0, (unsigned)BB, 0x00020000);
                 if (lane < NW) stage_block_169(stage, acc[j], lane);
@@ -768,7 +778,7 @@ __device__ __forceinline__ void gf_ring_run(
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
             const bool on = j < n;
-            const int oslot = (DECODE && slots) ? (on ? sload_u8(slots, g * rmax + j) : 0) : j;
+            const int oslot = (DECODE && slots) ? (on ? sload_u8(slots, g * rmax + j) : 0) : Y0 + j;
             uint8_t* dst = out + g * out_gstride + (long long)oslot * BB;
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(dst, 0, on ? (unsigned)BB : 0u, 0x00020000);
@@ -790,25 +800,56 @@ __device__ __forceinline__ void gf_ring_run(
     stream_wait_vmcnt<0>();
 }
 
-template <int K, int S, int RC, bool DECODE, int MC, bool NT = true, bool WIDE = false>
-__global__ __launch_bounds__(kRingWaves * 64) void gf_ring_kernel(
+#ifndef QF_RING_SKEW_INLINE
+#define QF_RING_SKEW_INLINE __forceinline__
+#endif
+#ifndef QF_RING_ATTR
+#define QF_RING_ATTR
+#endif
+template <int K, int S, int RC, bool DECODE, int MC, bool NT, bool WIDE, int NCH, int Y0>
+__device__ QF_RING_SKEW_INLINE void gf_ring_skew(
+    const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
+    const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
+    int rmax, long long coef_gstride, long long out_gstride, uint8_t* smem) {
+    if constexpr ((K * 8 * S) % 16 == 0) {
+        gf_ring_run<K, S, RC, DECODE, MC, NT, 0, WIDE, NCH, Y0>(in, out, coef, slots, nout, groups,
+                                                              rmax, coef_gstride, out_gstride, smem);
+    } else {
+        // group g starts 8 * (g & 1) bytes past a 16-byte boundary; a wave's groups g0,
+        // g0 + W, ... (W = 4 x the grid / NCH, even) all share g0's skew
+        const long long g0 = ((long long)blockIdx.x * kRingWaves + wave_id()) / NCH;
+        if (g0 & 1)
+            gf_ring_run<K, S, RC, DECODE, MC, NT, 8, WIDE, NCH, Y0>(in, out, coef, slots, nout,
+                                                                  groups, rmax, coef_gstride,
+                                                                  out_gstride, smem);
+        else
+            gf_ring_run<K, S, RC, DECODE, MC, NT, 0, WIDE, NCH, Y0>(in, out, coef, slots, nout,
+                                                                  groups, rmax, coef_gstride,
+                                                                  out_gstride, smem);
+    }
+}
+
+// NCH: parity-row chunks per group (encode; RC = MC / NCH rows each, chunk = the wave's unit
+// index mod NCH)
+template <int K, int S, int RC, bool DECODE, int MC, bool NT = true, bool WIDE = false, int NCH = 1>
+__global__ __launch_bounds__(kRingWaves * 64) QF_RING_ATTR void gf_ring_kernel(
     const uint8_t* in, uint8_t* out, const uint8_t* __restrict__ coef,
     const uint8_t* __restrict__ slots, const int32_t* __restrict__ nout, long long groups,
     int rmax, long long coef_gstride, long long out_gstride) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if constexpr ((K * 8 * S) % 16 == 0) {
-        gf_ring_run<K, S, RC, DECODE, MC, NT, 0, WIDE>(in, out, coef, slots, nout, groups, rmax,
-                                                  coef_gstride, out_gstride, smem);
+    static_assert(NCH == 1 || NCH == 2, "one or two chunks");
+    if constexpr (NCH == 1) {
+        gf_ring_skew<K, S, RC, DECODE, MC, NT, WIDE, 1, 0>(in, out, coef, slots, nout, groups,
+                                                         rmax, coef_gstride, out_gstride, smem);
     } else {
-        // group g starts 8 * (g & 1) bytes past a 16-byte boundary; a wave's groups g0,
-        // g0 + W, ... (W = 4 x the grid, even) all share g0's skew
-        const long long g0 = (long long)blockIdx.x * kRingWaves + wave_id();
-        if (g0 & 1)
-            gf_ring_run<K, S, RC, DECODE, MC, NT, 8, WIDE>(in, out, coef, slots, nout, groups, rmax,
-                                                      coef_gstride, out_gstride, smem);
+        if ((blockIdx.x * kRingWaves + wave_id()) & 1)
+            gf_ring_skew<K, S, RC, DECODE, MC, NT, WIDE, 2, RC>(in, out, coef, slots, nout,
+                                                              groups, rmax, coef_gstride,
+                                                              out_gstride, smem);
         else
-            gf_ring_run<K, S, RC, DECODE, MC, NT, 0, WIDE>(in, out, coef, slots, nout, groups, rmax,
-                                                      coef_gstride, out_gstride, smem);
+            gf_ring_skew<K, S, RC, DECODE, MC, NT, WIDE, 2, 0>(in, out, coef, slots, nout,
+                                                             groups, rmax, coef_gstride,
+                                                             out_gstride, smem);
     }
 }
 
@@ -927,16 +968,31 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         // 16, so the group's store count stays under the 63 a counted wait can name.  Not for
         // (10, 20): 290 VGPRs, one wave per SIMD (0.754 vs 0.673 ms); B/C keep 4 x 16 stores
         // 
-        const bool rwide = t.ring_wide && !(k == 32 && m == 4) && !(k == 10 && m == 20) &&
+        // (10, 20) in two units of 10 parity rows per group (ring_split): 10 accumulators
+        // per wave instead of 20, so wide stores fit the registers
+        const bool rsplit = t.ring_split && k == 10 && m == 20;
+        const bool rwide = t.ring_wide && !(k == 32 && m == 4) && (rsplit || !(k == 10 && m == 20)) &&
                            (((uintptr_t)out | (uintptr_t)out_gstride) & 7) == 0;
         const size_t rlds = (size_t)kRingWaves * (RingShape<169>::RB + (rwide ? kStreamStage : 0));
-        const long long rwant = (groups + kRingWaves - 1) / kRingWaves;
+        const long long rwant = (groups * (rsplit ? 2 : 1) + kRingWaves - 1) / kRingWaves;
         long long rcap = (long long)t.cus * (int)((160 * 1024) / rlds);
         if (t.stream_grid > 0) rcap = t.stream_grid;
         const unsigned rgrid = (unsigned)std::min<long long>(rwant, rcap);
-        if ((groups + (long long)rgrid * kRingWaves - 1) / ((long long)rgrid * kRingWaves) >=
+        if ((groups * (rsplit ? 2 : 1) + (long long)rgrid * kRingWaves - 1) / ((long long)rgrid * kRingWaves) >=
             (1LL << 31))
             return hipErrorInvalidValue;
+        if (rsplit) {
+            note_kernel("gf_ring_kernel<encode,k10m20,split>");
+            if (rwide)
+                qlaunch((gf_ring_kernel<10, 169, 10, false, 20, true, true, 2>), dim3(rgrid),
+                        dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax,
+                        coef_gstride, out_gstride);
+            else
+                qlaunch((gf_ring_kernel<10, 169, 10, false, 20, true, false, 2>), dim3(rgrid),
+                        dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax,
+                        coef_gstride, out_gstride);
+            return hipGetLastError();
+        }
 #define QR_GO1(KV, MCV, WV)                                                                     \
     qlaunch((gf_ring_kernel<KV, 169, MCV, false, MCV, true, WV>), dim3(rgrid),                   \
                        dim3(kRingWaves * 64), rlds, st, in, out, coef, slots, nout, groups, rmax, \

@@ -459,7 +459,7 @@ OPTION_SETS = [
     {"dma": 0}, {"stream": 0}, {"stream": 0, "pd": 1}, {"stream": 0, "pd": 3},
     {"stream": 0, "flat": 0}, {"enc_rc": 4}, {"enc_rc": 2}, {"prep_lane": 0},
     {"stream_ring": 36}, {"host_chunk_mb": 1, "host_min_groups": 1}, {"const_enc": 0},
-    {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 5}, {"bsyn_depth": 7},
+    {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 5}, {"bsyn_depth": 7}, {"ring_split": 0},
     {"dcol": 0}, {"dcol_depth": 8},
     {"psyn": 0},
 ]
