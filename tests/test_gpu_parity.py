@@ -724,7 +724,8 @@ def test_stream_any_small_block(engine, oracle, bb, k, m, r):
     recv = synth.assemble_received(data, p_or, src)
     b_or, r_or, s_or = oracle.decode_batch(k, m, bb, recv, rows)
     b, rr, s = gpu_decode(engine, k, m, bb, recv, rows, inplace=True)
-    dec = "gf_bsyn_kernel<decode" if (k, m, bb) == (32, 4, 1352) else "gf_stream_kernel<decode"
+    dec = ("gf_bsyn_kernel<decode" if (k, m, bb) == (32, 4, 1352) else
+           "gf_psyn_kernel<decode" if (k, m, bb) == (5, 5, 1352) else "gf_stream_kernel<decode")
     assert dec in fec.last_kernels()
     np.testing.assert_array_equal(s, s_or)
     np.testing.assert_array_equal(rr, r_or)

@@ -6,7 +6,7 @@ name=$1; tmo=$2; shift 2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 cd "$ROOT"
 GPU_STEPS_DRY=1 bash tools/gpu_steps.sh "$@" | while IFS= read -r spec; do
-  t="${spec%%::*}"; rm -rf "gpurun_out/$t.log" "gpurun_out/prof_$t"
+  t="${spec%%::*}"; rm -rf "gpurun_out/$t.log" "gpurun_out/prof_$t" gpurun_out/pmc_*_"$t" gpurun_out/pmc_*_"$t"_*.txt
 done
 q=""
 for s in "$@"; do q="$q '$s'"; done
