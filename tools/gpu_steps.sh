@@ -12,6 +12,7 @@
 #   preset:<k>,<m>        quick bench of a QuicR preset
 #   prof:<W>[:<args>]     rocprofv3 --kernel-trace --stats of a quick bench
 #   proflib:<name>,<W>[:<args>]  the same against quic_amd/libquic_fec_<name>.so
+#   profp:<k>,<m>[:<args>] rocprofv3 --kernel-trace --stats of a QuicR preset's quick bench
 #   abold:<W>[:<args>]    quick bench against quic_amd/libquic_fec_abold.so (an A/B build)
 #   libq:<name>,<W>[:<args>]  quick bench against quic_amd/libquic_fec_<name>.so (W = A..D or
 #                         P<k>_<m> for a QuicR preset)
@@ -52,6 +53,7 @@ for step in "$@"; do
     proflib) L="${W%%,*}"; WW="${W#*,}"
             case "$WW" in P*_*) wl="--preset ${WW#P}"; wl="${wl/_/,}" ;; *) wl="--workload $WW" ;; esac
             specs+=("$tag::300::QFEC_LIB_PATH=quic_amd/libquic_fec_$L.so rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run --output-format csv -- $quick $wl $extra") ;;
+    profp)  specs+=("$tag::300::rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run --output-format csv -- $quick --preset $W $extra") ;;
     pmc)    specs+=("$tag::600::bash tools/pmc.sh $W $tag $extra") ;;
     pmclib) L="${W%%,*}"; WW="${W#*,}"
             specs+=("$tag::600::QFEC_LIB_PATH=quic_amd/libquic_fec_$L.so bash tools/pmc.sh $WW $tag $extra") ;;
