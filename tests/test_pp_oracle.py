@@ -123,3 +123,26 @@ def test_batch_rejects_lengths_beyond_stride(oracle):
     _, res = oracle.null_open_batch(np.zeros((2, 32), np.uint8), np.array([33, 32], np.int32),
                                     np.array([0, 0], np.int32), 64)
     assert res[0] == -1 and res[1] == -1   # 33 > stride; 32 bytes: a bad tag
+
+
+def test_fnv_chain_split_algebra():
+    """The split DESIGN.md 6.2 plans for the FNV-1a chain, checked against the oracle's hash:
+    h ^ d = h + delta with delta = (l ^ d) - l, l = h mod 256, the low byte evolving alone as
+    l' = ((l ^ d) * 59) mod 256, so h_n = h_0 P^n + sum_i delta_i P^(n - i) (mod 2^96, the
+    tag's bits).  A plain restatement on the CPU (no GPU kernel implements it)."""
+    import numpy as np
+    from oracle import oracle as O
+    P, M96 = (1 << 88) + 315, (1 << 96) - 1
+    H0 = 144066263297769815596495629667062367629            # quic_utils.cc:116-118
+    rng = np.random.default_rng(5)
+    for n in [0, 1, 2, 17, 1380, 1999]:
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        lo, deltas = H0 & 255, []
+        for b in d.tolist():
+            x = lo ^ b
+            deltas.append(x - lo)
+            lo = (x * 59) & 255
+        h = H0 * pow(P, n, 1 << 96)
+        for i, dl in enumerate(deltas):
+            h += dl * pow(P, n - i, 1 << 96)
+        assert h & M96 == O.fnv1a_128(d) & M96, n
