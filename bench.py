@@ -396,8 +396,9 @@ def packet_protection(eng, k, m, bb, data, parity, steps, stream):
                         "packets in, recovered blocks out), wall clock per call, "
                         "H2D/kernels/D2H pipelined in chunks"},
             "note": "kernel-bracketing events per call; one lane per packet (serial FNV "
-                    "chain, six 22-bit limbs), DESIGN.md 6.2; open_decode loses data "
-                    "packet g % k of group g"}
+                    "chain mod 2^96 in three 32-bit words), packets streamed through "
+                    "LDS wave tiles, DESIGN.md 6.2; open_decode loses data packet "
+                    "g % k of group g"}
 
 
 def host_inclusive(eng, k, m, bb, payload, data, blocks, rows, steps, recovered):

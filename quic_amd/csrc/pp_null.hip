@@ -18,17 +18,13 @@
 // packets x 128 contiguous bytes each (chunk c of packet q at slot c ^ (q & 7), an XOR
 // swizzle so the lanes reading their own rows hit distinct banks); lane q hashes its packet's
 // valid bytes from LDS and writes each full 16-byte output line (realigned to the output's byte
-// phase, zeros past the source) back into the slot it consumed; then 8 coalesced non-temporal
+// phase, zeros past the source) back into the slot it consumed; then 8 coalesced
 // global_store_dwordx4 in the same shape.  The two partial output lines at a packet's ends are
-// written byte by byte after the loop, batched over the wave.  Then the tag.
+// written from registers after the loop.  Then the tag.
 //
-// The chain: h mod 2^96 (the tag is its low 96 bits) is kept as five 22-bit limbs in
-// carry-save form.  h * 315 is five full-rate 24-bit multiplies (v_mul_u32_u24; limbs 0..3
-// stay below 2^24, their products below 2^32), each limb keeps its low 22 bits and passes the
-// rest up one limb, and h << 88 mod 2^96 is one add of the low byte's limb into limb 4
-// (88 = 4 * 22; r05 kept six limbs, mod 2^128).  The low limb is always exact (nothing
-// carries into it), so the byte XOR is exact too; the limbs are normalised once, for the
-// tag.  Bound: the VALU and the chain's latency.
+// The chain: h mod 2^96 (the tag is its low 96 bits) in three 32-bit words, one 64-bit
+// multiply-add per word and byte (Fnv below).  Bound: the VALU of the chain and the tile's
+// LDS round trips at four to five waves per SIMD.
 //
 // Grouped forms (the FEC group's view of its packets): every data and FEC packet of G groups
 // sealed in one launch, and the receiver's open that writes each data packet's plaintext
@@ -46,31 +42,28 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // FNV-1a-128 modulo 2^96: the tag is the low 96 bits of the hash (quic_utils.cc:175-181,
 // null_encrypter.cc:23-43; the decrypter compares the same bits), and arithmetic mod 2^128
-// reduces to arithmetic mod 2^96, so bits 96..127 are never formed.  Five 22-bit limbs (limb j
-// = bits 22j ..), carry-save: limbs 1..3 may exceed 22 bits by the carry they received (< 2^24
-// always); limb 4 (bits 88..) is kept unmasked, only its low 8 bits count.  h * P =
-// h * 315 + (h << 88): mod 2^96 the shifted term is the low byte of h ^ byte added to limb 4.
+// reduces to arithmetic mod 2^96, so bits 96..127 are never formed.  h is three 32-bit words;
+// h * P = h * 315 + (h << 88): h * 315 is one 32 x 32 -> 64-bit multiply-add per word
+// (v_mad_u64_u32; the low word's high half carries into the next, the top word's product is
+// kept mod 2^32), and (h ^ byte) << 88 mod 2^96 is the XORed low byte shifted into bits 24..31
+// of the top word.  About 8 VALU per byte, where r02-r06's five 22-bit limbs in carry-save form
+// (v_mul_u32_u24 per limb, masks and shifts between) took 17; the chain alone runs 2.4x as
+// fast (tools/microbench/fnv_rate.hip).
 struct Fnv {
-    uint32_t l0, l1, l2, l3, l4;
-    // kOffset = 144066263297769815596495629667062367629 (quic_utils.cc:116-118), low 96 bits
+    uint32_t h0, h1, h2;
+    // kOffset = 144066263297769815596495629667062367629 (quic_utils.cc:116-118) mod 2^96
     __device__ __forceinline__ void init() {
-        l0 = 0x15c58du;
-        l1 = 0x05d58au;
-        l2 = 0x262b82u;
-        l3 = 0x2ec050u;
-        l4 = 0x272e07u;
+        h0 = 0x6295C58Du;
+        h1 = 0x62B82175u;
+        h2 = 0x07BB0142u;
     }
     __device__ __forceinline__ void byte(uint32_t b) {
-        constexpr uint32_t M = (1u << 22) - 1u;
-        const uint32_t x0 = l0 ^ b;   // l0 < 2^22 is exact: the XOR is the reference's
-        const uint32_t p0 = __umul24(x0, 315u), p1 = __umul24(l1, 315u);
-        const uint32_t p2 = __umul24(l2, 315u), p3 = __umul24(l3, 315u);
-        const uint32_t p4 = __umul24(l4, 315u);   // low 24 bits of l4: its low 8 are exact
-        l4 = p4 + (p3 >> 22) + x0;                // + (h << 88) mod 2^96
-        l1 = (p1 & M) + (p0 >> 22);
-        l2 = (p2 & M) + (p1 >> 22);
-        l3 = (p3 & M) + (p2 >> 22);
-        l0 = p0 & M;
+        const uint32_t x0 = h0 ^ b;
+        const uint64_t p0 = (uint64_t)x0 * 315u;
+        const uint64_t p1 = (uint64_t)h1 * 315u + (p0 >> 32);
+        h2 = h2 * 315u + (uint32_t)(p1 >> 32) + (x0 << 24);
+        h0 = (uint32_t)p0;
+        h1 = (uint32_t)p1;
     }
     __device__ __forceinline__ void word(uint32_t w) {
         byte(w & 0xFFu);
@@ -80,22 +73,18 @@ struct Fnv {
     }
     // the low 96 bits of h, little-endian dwords (SerializeUint128Short, quic_utils.cc:175-181)
     __device__ __forceinline__ void tag(uint32_t& t0, uint32_t& t1, uint32_t& t2) const {
-        constexpr uint32_t M = (1u << 22) - 1u;
-        uint32_t c = 0, n[5];
-        const uint32_t l[5] = {l0, l1, l2, l3, l4};
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const uint32_t v = l[j] + c;
-            n[j] = v & M;
-            c = v >> 22;
-        }
-        const uint64_t lo = (uint64_t)n[0] | ((uint64_t)n[1] << 22) | ((uint64_t)n[2] << 44);
-        const uint32_t hi = (n[2] >> 20) | (n[3] << 2) | (n[4] << 24);
-        t0 = (uint32_t)lo;
-        t1 = (uint32_t)(lo >> 32);
-        t2 = hi;
+        t0 = h0, t1 = h1, t2 = h2;
     }
 };
+
+// stores through the global address space (a generic pointer compiles to flat stores, which
+// also count on the LDS counter that tile_stream's waits after each ds_read use)
+__device__ __forceinline__ void gst32(uint8_t* a, uint32_t v) {
+    *(__attribute__((address_space(1))) uint32_t*)(uintptr_t)a = v;
+}
+__device__ __forceinline__ void gst8(uint8_t* a, uint32_t v) {
+    *(__attribute__((address_space(1))) uint8_t*)(uintptr_t)a = (uint8_t)v;
+}
 
 // Per-lane byte-stream writer: bytes go out as aligned dword stores; `carry` holds the bytes
 // of the current dword not yet stored.  Bytes before `start` are not the writer's: a dword
@@ -110,9 +99,9 @@ struct Sink {
     }
     __device__ __forceinline__ void store_dw(uint8_t* a, uint32_t v) {   // a 4-byte aligned
         if (a >= start) {
-            *(uint32_t*)a = v;
+            gst32(a, v);
         } else {
-            for (int q = (int)(start - a); q < 4; ++q) a[q] = (uint8_t)(v >> (8 * q));
+            for (int q = (int)(start - a); q < 4; ++q) gst8(a + q, v >> (8 * q));
         }
     }
     __device__ __forceinline__ void word(uint32_t w) {
@@ -135,7 +124,7 @@ struct Sink {
         const uint32_t pb = (uint32_t)(uintptr_t)ptr & 3u;
         uint8_t* a = ptr - pb;
         for (uint32_t q = 0; q < pb; ++q)
-            if (a + q >= start) a[q] = (uint8_t)(carry >> (8 * q));
+            if (a + q >= start) gst8(a + q, carry >> (8 * q));
     }
     // zero bytes up to `end`, then flush
     __device__ __forceinline__ void zeros_to(const uint8_t* end) {
@@ -150,7 +139,7 @@ struct Sink {
 // 16-byte loads with the next chunk in flight while this one is consumed, then the last
 // < 64 bytes.  HASH: into h; WRITE: through s.
 constexpr int CH = 4;
-template <bool HASH, bool WRITE, class H>
+template <bool HASH, bool WRITE, int CHN = CH, class H>
 __device__ __forceinline__ void span(H& h, Sink& s, const uint8_t* p, int len) {
     if (len <= 0) return;
     auto dw = [&](uint32_t w) {
@@ -171,7 +160,7 @@ __device__ __forceinline__ void span(H& h, Sink& s, const uint8_t* p, int len) {
     for (int i = 0; i < head; ++i) by(p[i]);
     const u32x4* q = (const u32x4*)(p + head);
     const int rest = len - head;
-    const int nc = rest >> 6;   // 64-byte chunks
+    const int nc = rest / (16 * CHN);   // 16 * CHN-byte chunks
     // Line writer for the chunks: 16 source bytes make 4 output dwords d0..d3 (realigned by
     // pb = ptr % 4 bytes with the carry), which land at dword positions di..di+3 of the
     // output's 16-byte lines (di = the dword index of ptr - pb in its line, fixed for the
@@ -221,34 +210,34 @@ __device__ __forceinline__ void span(H& h, Sink& s, const uint8_t* p, int len) {
                 o.y = di > 1 ? P1 : d1;
                 o.z = di > 2 ? P2 : d2;
                 o.w = d3;
-                *(u32x4*)line = o;
+                *(__attribute__((address_space(1))) u32x4*)(uintptr_t)line = o;
             }
             P0 = d0, P1 = d1, P2 = d2, P3 = d3;
             s.carry = nc4;
             s.ptr += 16;
         }
     };
-    u32x4 a[CH], b[CH];
+    u32x4 a[CHN], b[CHN];
     if (nc > 0) {
 #pragma unroll
-        for (int u = 0; u < CH; ++u) a[u] = __builtin_nontemporal_load(q + u);
+        for (int u = 0; u < CHN; ++u) a[u] = __builtin_nontemporal_load(q + u);
     }
     for (int j = 0; j < nc; j += 2) {
         if (j + 1 < nc) {
 #pragma unroll
-            for (int u = 0; u < CH; ++u) b[u] = __builtin_nontemporal_load(q + CH * (j + 1) + u);
+            for (int u = 0; u < CHN; ++u) b[u] = __builtin_nontemporal_load(q + CHN * (j + 1) + u);
         }
         eat4(a[0], j == 0);
 #pragma unroll
-        for (int u = 1; u < CH; ++u) eat4(a[u], false);
+        for (int u = 1; u < CHN; ++u) eat4(a[u], false);
         if (j + 1 < nc) {
             if (j + 2 < nc) {
 #pragma unroll
-                for (int u = 0; u < CH; ++u)
-                    a[u] = __builtin_nontemporal_load(q + CH * (j + 2) + u);
+                for (int u = 0; u < CHN; ++u)
+                    a[u] = __builtin_nontemporal_load(q + CHN * (j + 2) + u);
             }
 #pragma unroll
-            for (int u = 0; u < CH; ++u) eat4(b[u], false);
+            for (int u = 0; u < CHN; ++u) eat4(b[u], false);
         }
     }
     if constexpr (WRITE) {
@@ -261,8 +250,8 @@ __device__ __forceinline__ void span(H& h, Sink& s, const uint8_t* p, int len) {
         }
     }
     (void)P3;
-    const u32x4* r = q + CH * nc;
-    const int nr = (rest & 63) >> 4;
+    const u32x4* r = q + CHN * nc;
+    const int nr = (rest % (16 * CHN)) >> 4;
 #pragma unroll 1
     for (int u = 0; u < nr; ++u) eat(__builtin_nontemporal_load(r + u));
     const uint8_t* tb = (const uint8_t*)(r + nr);
@@ -280,18 +269,24 @@ __device__ __forceinline__ int len_of(const int32_t* a, int all, long long i) {
 // touched 64 cache lines per instruction and cost 1.4x the reads (L2 re-fetches) and 1.55x
 // the writes (partial lines) of the one-lane-per-packet streamer (profiles/r05/pp/).  Each lane
 // still owns its packet's serial FNV chain.
-//   window w of packet q: source chunks 8w .. 8w + 7 (16 bytes each, from its 16-byte aligned
-//   start); the tile row of packet q is 128 bytes at q * 128, chunk c at slot c ^ (q & 7) (an
-//   XOR swizzle: lanes reading their rows at one chunk index hit distinct banks).
+//   window w of packet q: source chunks 8w .. 8w + 7 (16 bytes each) counted from the source's
+//   128-byte aligned line, so that a window is one whole cache line; the tile row of packet q
+//   is 128 bytes at q * 128, chunk c at slot c ^ (q & 7) (an XOR swizzle: lanes reading their
+//   rows at one chunk index hit distinct banks).
 //   1. loads: 8 global_load_lds_dwordx4 (instruction j: packets 8j .. 8j + 7, lane = 8 (q % 8)
 //      + slot), each lane's address from its packet's lane by ds_bpermute;
 //   2. lane q reads its 8 chunks, hashes the valid bytes, and writes each FULL 16-byte output
 //      line (realigned to the output's phase, zeros past the source) back into the slot of the
-//      chunk it just consumed;
-//   3. stores: 8 global_store_dwordx4 in the same shape (full lines only).
-// The partial output lines at the two ends (< 16 bytes each) are written byte by byte.
-// Measured variants: 64-byte windows double-buffered, and two packets
-// per lane (two interleaved chains) with 64-byte windows, were both slower.
+//      chunk it just consumed; the partial lines at the output's two ends stay in registers;
+//   3. stores: 8 global_store_dwordx4 in the same shape (full lines only), plain stores: the
+//      window's first and last lines share cache lines with the neighbouring windows, and L2
+//      merges those partial writes; non-temporal stores sent them to HBM half-filled (r06:
+//      1.13 -> 0.73 ms for all of A's packets).
+// After the last window, the two partial end lines are written from registers, whole dwords
+// where the output covers them.
+// Measured and not kept: 64-byte windows double-buffered, two packets
+// per lane, 16-byte aligned windows (each window straddled two lines), and (r06) two window
+// buffers with the next window's DMA in flight during the hash (64- and 128-byte windows).
 constexpr int kTileBytes = 64 * 128;   // one wave's tile
 constexpr int kTilePackets = 64;       // packets per wave (one per lane)
 
@@ -306,25 +301,61 @@ __device__ __forceinline__ int wave_max(int v) {
     for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
     return v;
 }
-// A[idx] for a per-lane idx in 0..7
-__device__ __forceinline__ uint32_t pick8(const uint32_t (&A)[8], int idx) {
-    const uint32_t a0 = (idx & 1) ? A[1] : A[0], a1 = (idx & 1) ? A[3] : A[2];
-    const uint32_t a2 = (idx & 1) ? A[5] : A[4], a3 = (idx & 1) ? A[7] : A[6];
-    const uint32_t b0 = (idx & 2) ? a1 : a0, b1 = (idx & 2) ? a3 : a2;
-    return (idx & 4) ? b1 : b0;
+
+// The output line at per-lane dword offset mi (0..4) and byte offset ri (0..3) into the 32
+// bytes P || C (the previous chunk, this chunk): dword t = bytes 4 (mi + t) + ri .. + 3, dwords
+// past the pair clamped to C[3].  The five dwords it needs are selected by the bits of mi in
+// three steps, then realigned by ri.
+__device__ __forceinline__ u32x4 line_of(const uint32_t (&P)[4], const uint32_t (&C)[4], int mi,
+                                         int ri) {
+    // bitwise selects: a conditional between array elements would be folded into one load
+    // with a computed index, which puts the array in scratch memory
+    const uint32_t A[8] = {P[0], P[1], P[2], P[3], C[0], C[1], C[2], C[3]};
+    const uint32_t m0 = 0u - (uint32_t)(mi & 1), m1 = 0u - (uint32_t)((mi >> 1) & 1);
+    const uint32_t m2 = 0u - (uint32_t)((mi >> 2) & 1);
+    uint32_t B[7], Q[5], V[5];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) B[t] = (A[t + 1] & m0) | (A[t] & ~m0);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) Q[t] = (B[t + 2] & m1) | (B[t] & ~m1);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) V[t] = (A[min(4 + t, 7)] & m2) | (Q[t] & ~m2);
+    u32x4 o;
+    o.x = __builtin_amdgcn_alignbyte(V[1], V[0], ri);
+    o.y = __builtin_amdgcn_alignbyte(V[2], V[1], ri);
+    o.z = __builtin_amdgcn_alignbyte(V[3], V[2], ri);
+    o.w = __builtin_amdgcn_alignbyte(V[4], V[3], ri);
+    return o;
+}
+
+// bytes [lo, hi) of the 16-byte line at L (16-byte aligned) from o: dword stores for the
+// dwords inside the range, byte stores for the rest
+__device__ __forceinline__ void part_line(uint8_t* L, const uint32_t (&o)[4], int lo, int hi) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        if (lo <= 4 * t && 4 * t + 4 <= hi) {
+            gst32(L + 4 * t, o[t]);
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (lo <= 4 * t + b && 4 * t + b < hi) gst8(L + 4 * t + b, o[t] >> (8 * b));
+        }
+    }
 }
 
 // Hash pl source bytes at src into h and write them to dst, followed by zeros up to olen
 // bytes (olen == 0: hash only).  Called by every lane of the wave together (wave-uniform
 // loop); a lane with pl == 0 and olen == 0 only takes part.  tile: this wave's kTileBytes of
-// LDS.  Every memory access of the routine is complete when it returns.
+// LDS.  Every memory access of the routine is complete when it returns.  The first window
+// starts at the source's 128-byte aligned line: the bytes before src that it loads lie in
+// that line (never another page) and are neither hashed nor written.
 template <class H>
 __device__ void tile_stream(H& h, const uint8_t* src, int pl, uint8_t* dst, int olen,
                             uint8_t* tile) {
     const int lane = (int)__lane_id();
     const uintptr_t sp = (uintptr_t)src;
-    const int hoff = pl > 0 ? (int)(sp & 15u) : 0;
-    const uint64_t s16 = (uint64_t)(sp - hoff);
+    const int hoff = pl > 0 ? (int)(sp & 127u) : 0;
+    const uint64_t s128 = (uint64_t)(sp - hoff);
     const int cmax = pl > 0 ? (hoff + pl - 1) >> 4 : -1;   // last chunk holding a source byte
     const int send = hoff + pl;                             // source end, chunk coordinates
     // output: stream byte x goes to D + x, D = dst - hoff; 16-byte lines from A0 = D rounded
@@ -337,12 +368,17 @@ __device__ void tile_stream(H& h, const uint8_t* src, int pl, uint8_t* dst, int 
         jf = (int)(((uint64_t)(uintptr_t)dst - A0 + 15u) >> 4);
         jl = (int)(((uint64_t)(uintptr_t)dst + (uint64_t)olen - A0) >> 4) - 1;
     }
-    const int last = max(cmax, jl);
+    // the partial output lines at the two ends: line jf - 1 (when dst is inside it) and line
+    // jl + 1 (when the output ends inside it); the same line when the output lies in one line
+    const bool hpart = olen > 0 && (uint64_t)(uintptr_t)dst != A0 + 16u * (uint64_t)jf;
+    const bool tpart = olen > 0 && (uint64_t)(uintptr_t)dst + (uint64_t)olen != A0 + 16u * (uint64_t)(jl + 1);
+    const int last = max(cmax, tpart ? jl + 1 : jl);
     const int nwin_l = last >= 0 ? (last >> 3) + 1 : 0;
     const int nwin = wave_max(nwin_l);
     // line g = stream bytes [16 g - e, 16 g - e + 16): from (previous chunk, this chunk)
     const int mi = (16 - e) >> 2, ri = (16 - e) & 3;
     uint32_t P[4] = {0u, 0u, 0u, 0u};
+    uint32_t Hd[4] = {0u, 0u, 0u, 0u}, Tl[4] = {0u, 0u, 0u, 0u};
     const int lq = lane >> 3, pos = lane & 7;
     const int rowoff = lane * 128, sw = lane & 7;
     const uint32_t tb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)tile;
@@ -352,24 +388,24 @@ __device__ void tile_stream(H& h, const uint8_t* src, int pl, uint8_t* dst, int 
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int q = 8 * j + lq;
-            const uint64_t qs = bperm64(s16, q);
+            const uint64_t qs = bperm64(s128, q);
             const int qc = (int)bperm((uint32_t)cmax, q);
             const int cg = 8 * w + (pos ^ (q & 7));
             if (cg <= qc)
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void*)(uintptr_t)(qs + 16u * (uint64_t)cg),
-                    (__attribute__((address_space(3))) void*)(tile + 1024 * j), 16, 0, 2);
+                    (__attribute__((address_space(3))) void*)(tile + 1024 * j), 16, 0, 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        // 2. this lane's row: hash, and full output lines back into the tile
+        // 2. this lane's row: hash, full output lines back into the tile, end lines kept
         if (w < nwin_l) {
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 const int g = 8 * w + c;
                 const uint32_t a = tb + (uint32_t)(rowoff + ((c ^ sw) << 4));
                 uint32_t C[4] = {0u, 0u, 0u, 0u};
-                if (g <= cmax) {
+                if (g <= cmax && 16 * g + 16 > hoff) {   // chunks before the source stay zero
                     u32x4 v;
                     asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
                     C[0] = v.x, C[1] = v.y, C[2] = v.z, C[3] = v.w;
@@ -391,14 +427,13 @@ __device__ void tile_stream(H& h, const uint8_t* src, int pl, uint8_t* dst, int 
                         }
                     }
                 }
-                if (g >= jf && g <= jl) {
-                    const uint32_t A[8] = {P[0], P[1], P[2], P[3], C[0], C[1], C[2], C[3]};
-                    u32x4 o;
-                    o.x = __builtin_amdgcn_alignbyte(pick8(A, min(mi + 1, 7)), pick8(A, mi), ri);
-                    o.y = __builtin_amdgcn_alignbyte(pick8(A, min(mi + 2, 7)), pick8(A, min(mi + 1, 7)), ri);
-                    o.z = __builtin_amdgcn_alignbyte(pick8(A, min(mi + 3, 7)), pick8(A, min(mi + 2, 7)), ri);
-                    o.w = __builtin_amdgcn_alignbyte(pick8(A, min(mi + 4, 7)), pick8(A, min(mi + 3, 7)), ri);
-                    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(o) : "memory");
+                const bool full = g >= jf && g <= jl;
+                const bool hl = hpart && g == jf - 1, tl = tpart && g == jl + 1;
+                if (full || hl || tl) {
+                    const u32x4 o = line_of(P, C, mi, ri);
+                    if (hl) Hd[0] = o.x, Hd[1] = o.y, Hd[2] = o.z, Hd[3] = o.w;
+                    if (tl) Tl[0] = o.x, Tl[1] = o.y, Tl[2] = o.z, Tl[3] = o.w;
+                    if (full) asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(o) : "memory");
                 }
 #pragma unroll
                 for (int t = 0; t < 4; ++t) P[t] = C[t];
@@ -417,28 +452,19 @@ __device__ void tile_stream(H& h, const uint8_t* src, int pl, uint8_t* dst, int 
                 const uint32_t a = tb + (uint32_t)(q * 128 + ((pos ^ (q & 7)) << 4));
                 u32x4 v;
                 asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-                __builtin_nontemporal_store(v, (u32x4*)(uintptr_t)(qa + 16u * (uint64_t)g));
+                *(__attribute__((address_space(1))) u32x4*)(uintptr_t)(qa + 16u * (uint64_t)g) = v;
             }
         }
         __builtin_amdgcn_wave_barrier();
     }
-    // 4. the partial lines at both ends, byte by byte: at most 15 bytes each, or the whole
-    // output (< 32 bytes) when it has no full line; all loads in flight before the stores
-    if (olen > 0) {
-        const int nh = jl >= jf ? (int)(A0 + 16u * (uint64_t)jf - (uint64_t)(uintptr_t)dst) : olen;
-        const int tb0 = jl >= jf ? (int)(A0 + 16u * (uint64_t)(jl + 1) - (uint64_t)(uintptr_t)dst) : olen;
-        const int nt = olen - tb0;
-        uint32_t hv[32], tv[16];
-#pragma unroll
-        for (int i = 0; i < 32; ++i) hv[i] = (i < nh && i < pl) ? src[i] : 0u;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) tv[i] = (i < nt && tb0 + i < pl) ? src[tb0 + i] : 0u;
-#pragma unroll
-        for (int i = 0; i < 32; ++i)
-            if (i < nh) dst[i] = (uint8_t)hv[i];
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-            if (i < nt) dst[tb0 + i] = (uint8_t)tv[i];
+    // 4. the partial lines at both ends, from registers
+    if (hpart) {
+        uint8_t* L = (uint8_t*)(uintptr_t)(A0 + 16u * (uint64_t)(jf - 1));
+        part_line(L, Hd, (int)(dst - L), min(16, (int)(dst + olen - L)));
+    }
+    if (tpart && !(hpart && jl + 1 == jf - 1)) {
+        uint8_t* L = (uint8_t*)(uintptr_t)(A0 + 16u * (uint64_t)(jl + 1));
+        part_line(L, Tl, max(0, (int)(dst - L)), (int)(dst + olen - L));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -497,7 +523,7 @@ __global__ __launch_bounds__(64) void null_seal_kernel(
     h.init();
     Sink s, t;
     s.begin(o);
-    if (ok) span<true, true>(h, s, ad + i * ad_stride, al);
+    if (ok) span<true, true, 1>(h, s, ad + i * ad_stride, al);   // a few bytes: 16-byte pieces
     t = s;   // AD's unstored tail bytes; the tag follows them once it is known
     tile_stream(h, ok ? pt_row(pr, i) : nullptr, ok ? pl : 0, o + al + 12, ok ? pl : 0, smem);
     if (!ok) return;
@@ -584,7 +610,7 @@ __global__ __launch_bounds__(64) void open_group_kernel(
     H h;
     h.init();
     Sink s;
-    if (ok) span<true, false>(h, s, pp, al);
+    if (ok) span<true, false, 1>(h, s, pp, al);
     const bool data = ok && i < k;
     tile_stream(h, ok ? c + 12 : nullptr, ok ? cl - 12 : 0,
                 data ? blocks + (g * k + i) * (long long)bb : nullptr, data ? bb : 0, smem);
@@ -702,7 +728,6 @@ unsigned tile_grid(long long n) {   // one wave (kTilePackets packets) per workg
 
 }  // namespace
 
-// the six-limb FNV chain (a 64-bit-halves form measured within 3 % and was removed, r05)
 #define QPP_GO(KERNEL, ...) qlaunch(KERNEL<Fnv>, __VA_ARGS__)
 
 hipError_t launch_null_seal_h(long long n, const uint8_t* ad, long long ad_stride,

@@ -5,6 +5,8 @@
 # time limit, see tools/gpu_session.sh):
 #   tests                 the whole -m gpu suite
 #   tests:<file|-k expr>  one test file (tests/test_gpu_pp.py) or a -k selection
+#   testlib:<name>,<file> one test file against quic_amd/libquic_fec_<name>.so
+#   mb:<name>             the microbenchmark binary tools/microbench/<name>
 #   smoke                 __graft_entry__.smoke()
 #   default               python bench.py (the driver's round-end line)
 #   bench:<W>[:<args>]    bench.py --workload W --verify (W = A B C D), extra args after ':'
@@ -39,6 +41,9 @@ for step in "$@"; do
       elif [ -f "$rest" ]; then sel="$rest"
       else sel="tests -k '$rest'"; fi
       specs+=("$tag::900::python -u -m pytest $sel -m gpu -x -q --timeout 120 --timeout-method thread") ;;
+    testlib) L="${W%%,*}"; F="${W#*,}"
+            specs+=("$tag::900::QFEC_LIB_PATH=quic_amd/libquic_fec_$L.so python -u -m pytest $F -m gpu -x -q --timeout 120 --timeout-method thread") ;;
+    mb)     specs+=("$tag::120::tools/microbench/$W") ;;
     default) specs+=("default::600::python bench.py") ;;
     smoke)  specs+=("smoke::300::python -c 'import __graft_entry__ as g; g.smoke()'") ;;
     bench)  specs+=("$tag::600::python bench.py --workload $W --verify $extra") ;;
