@@ -279,9 +279,9 @@ __device__ __forceinline__ int len_of(const int32_t* a, int all, long long i) {
 //      line (realigned to the output's phase, zeros past the source) back into the slot of the
 //      chunk it just consumed; the partial lines at the output's two ends stay in registers;
 //   3. stores: 8 global_store_dwordx4 in the same shape (full lines only), plain stores: the
-//      window's first and last lines share cache lines with the neighbouring windows, and L2
-//      merges those partial writes; non-temporal stores sent them to HBM half-filled (r06:
-//      1.13 -> 0.73 ms for all of A's packets).
+//      next window's vmcnt(0) waits for them too, and non-temporal stores were acknowledged
+//      later for the same bytes written (r06: 1.13 -> 0.73 ms for all of A's packets, WRITE_SIZE
+//      unchanged).
 // After the last window, the two partial end lines are written from registers, whole dwords
 // where the output covers them.
 // Measured and not kept: 64-byte windows double-buffered, two packets
