@@ -220,7 +220,8 @@ QFEC_API int qfec_encode_seal_groups_batch(qfec_ctx *ctx, int k, int m, int bloc
  *                        data packet did not open holds the plaintext of the next opened FEC
  *                        packet (ascending)
  *   d_rows [G][k]        the row tag of each slot (i, or k + j for FEC packet j; 255 when no
- *                        opened FEC packet is left, and the group's status is then -3)
+ *                        opened FEC packet is left, and the group's status is then -3; the
+ *                        bytes of a slot tagged 255 are unspecified)
  * followed by qfec_decode_batch_recovered(d_blocks, d_rows) into d_rec / d_rec_rows /
  * d_status (a group with an unfilled slot: status -3, recovered rows all 255).  Four
  * launches on one stream.  k + m <= 255. */

@@ -274,11 +274,13 @@ __device__ __forceinline__ int len_of(const int32_t* a, int all, long long i) {
 //   is 128 bytes at q * 128, chunk c at slot c ^ (q & 7) (an XOR swizzle: lanes reading their
 //   rows at one chunk index hit distinct banks).
 //   1. loads: 8 global_load_lds_dwordx4 (instruction j: packets 8j .. 8j + 7, lane = 8 (q % 8)
-//      + slot), each lane's address from its packet's lane by ds_bpermute;
+//      + slot), each lane's address from its packet's lane by ds_bpermute (all 8 exchanges
+//      issued before the first load, so their latency is paid once, not 8 times);
 //   2. lane q reads its 8 chunks, hashes the valid bytes, and writes each FULL 16-byte output
 //      line (realigned to the output's phase, zeros past the source) back into the slot of the
 //      chunk it just consumed; the partial lines at the output's two ends stay in registers;
-//   3. stores: 8 global_store_dwordx4 in the same shape (full lines only), plain stores: the
+//   3. stores: 8 global_store_dwordx4 in the same shape (full lines only; exchanges and LDS
+//      reads four instructions at a time), plain stores: the
 //      next window's vmcnt(0) waits for them too, and non-temporal stores were acknowledged
 //      later for the same bytes written (r06: 1.13 -> 0.73 ms for all of A's packets, WRITE_SIZE
 //      unchanged).
@@ -385,16 +387,23 @@ __device__ void tile_stream(H& h, const uint8_t* src, int pl, uint8_t* dst, int 
 #pragma unroll 1
     for (int w = 0; w < nwin; ++w) {
         // 1. coalesced loads: instruction j brings packets 8j .. 8j + 7
+        {
+            uint64_t qs[8];
+            int qc[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int q = 8 * j + lq;
-            const uint64_t qs = bperm64(s128, q);
-            const int qc = (int)bperm((uint32_t)cmax, q);
-            const int cg = 8 * w + (pos ^ (q & 7));
-            if (cg <= qc)
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(uintptr_t)(qs + 16u * (uint64_t)cg),
-                    (__attribute__((address_space(3))) void*)(tile + 1024 * j), 16, 0, 0);
+            for (int j = 0; j < 8; ++j) {   // every exchange first: one wait for all of them
+                qs[j] = bperm64(s128, 8 * j + lq);
+                qc[j] = (int)bperm((uint32_t)cmax, 8 * j + lq);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int q = 8 * j + lq;
+                const int cg = 8 * w + (pos ^ (q & 7));
+                if (cg <= qc[j])
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)(uintptr_t)(qs[j] + 16u * (uint64_t)cg),
+                        (__attribute__((address_space(3))) void*)(tile + 1024 * j), 16, 0, 0);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
@@ -443,16 +452,25 @@ __device__ void tile_stream(H& h, const uint8_t* src, int pl, uint8_t* dst, int 
         __builtin_amdgcn_wave_barrier();
         // 3. coalesced stores of the full lines: instruction j, packets 8j .. 8j + 7
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int q = 8 * j + lq;
-            const int qf = (int)bperm((uint32_t)jf, q), ql = (int)bperm((uint32_t)jl, q);
-            const uint64_t qa = bperm64(A0, q);
-            const int g = 8 * w + pos;
-            if (g >= qf && g <= ql) {
+        for (int h4 = 0; h4 < 8; h4 += 4) {   // four instructions at a time: exchanges and
+            int qf[4], ql[4];                  // LDS reads issued together, one wait each
+            uint64_t qa[4];
+            u32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = 8 * (h4 + u) + lq;
+                qf[u] = (int)bperm((uint32_t)jf, q);
+                ql[u] = (int)bperm((uint32_t)jl, q);
+                qa[u] = bperm64(A0, q);
                 const uint32_t a = tb + (uint32_t)(q * 128 + ((pos ^ (q & 7)) << 4));
-                u32x4 v;
-                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-                *(__attribute__((address_space(1))) u32x4*)(uintptr_t)(qa + 16u * (uint64_t)g) = v;
+                asm volatile("ds_read_b128 %0, %1" : "=v"(v[u]) : "v"(a) : "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int g = 8 * w + pos;
+                if (g >= qf[u] && g <= ql[u])
+                    *(__attribute__((address_space(1))) u32x4*)(uintptr_t)(qa[u] + 16u * (uint64_t)g) = v[u];
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -584,8 +602,41 @@ __global__ __launch_bounds__(kPPThreads) void null_open_kernel(
     out_len[i] = res;
 }
 
+// The open's length checks alone (the tag is checked later): a packet that fails them is
+// rejected whatever its bytes.
+__device__ __forceinline__ bool open_len_ok(const int32_t* __restrict__ pkt_len,
+                                            const int32_t* __restrict__ ad_len, int ad_all,
+                                            long long p, int bb, long long pkt_stride) {
+    const int tl = pkt_len[p];
+    const int al = len_of(ad_len, ad_all, p);
+    const int cl = tl - al;
+    return tl >= 0 && al >= 0 && cl >= 12 && cl - 12 <= bb && tl <= pkt_stride;
+}
+
+// The slot FEC packet i (>= k) of group g is written to by the open, before any tag is known:
+// the holes and the available FEC packets as the length checks alone leave them, matched in
+// ascending order as open_assemble_kernel matches them (the j-th available FEC packet fills
+// the j-th hole); -1 when it fills none.  Where a tag check then changes the match,
+// open_assemble_kernel copies the right packet over.
+__device__ int fec_pre_slot(const int32_t* __restrict__ pkt_len,
+                            const int32_t* __restrict__ ad_len, int ad_all, long long g, int i,
+                            int k, int m, int bb, long long pkt_stride) {
+    const long long p0 = g * (k + m);
+    int j = 0;
+#pragma unroll 4
+    for (int q = k; q < i; ++q) j += open_len_ok(pkt_len, ad_len, ad_all, p0 + q, bb, pkt_stride) ? 1 : 0;
+#pragma unroll 8
+    for (int x = 0; x < k; ++x) {
+        if (open_len_ok(pkt_len, ad_len, ad_all, p0 + x, bb, pkt_stride)) continue;
+        if (j == 0) return x;
+        --j;
+    }
+    return -1;
+}
+
 // Receiver, grouped: packet p = g * (k + m) + i, one wave per 64 packets; a data packet's
-// plaintext goes to its block slot, zero-padded to bb, through the wave's LDS tile.
+// plaintext goes to its block slot, zero-padded to bb, through the wave's LDS tile, and so
+// does an FEC packet's, into the hole it fills if the tags change nothing (fec_pre_slot).
 template <class H>
 __global__ __launch_bounds__(64) void open_group_kernel(
     int k, int m, int bb, long long n, const uint8_t* __restrict__ pkt, long long pkt_stride,
@@ -611,9 +662,11 @@ __global__ __launch_bounds__(64) void open_group_kernel(
     h.init();
     Sink s;
     if (ok) span<true, false, 1>(h, s, pp, al);
-    const bool data = ok && i < k;
+    const int slot = !ok ? -1 : i < k ? i
+                   : fec_pre_slot(pkt_len, ad_len, ad_all, g, i, k, m, bb, pkt_stride);
     tile_stream(h, ok ? c + 12 : nullptr, ok ? cl - 12 : 0,
-                data ? blocks + (g * k + i) * (long long)bb : nullptr, data ? bb : 0, smem);
+                slot >= 0 ? blocks + (g * k + slot) * (long long)bb : nullptr, slot >= 0 ? bb : 0,
+                smem);
     if (!ok) return;
     uint32_t t0, t1, t2;
     h.tag(t0, t1, t2);
@@ -646,13 +699,16 @@ __device__ void wave_copy_pad(uint8_t* dst, const uint8_t* src, int pl, int bb, 
 constexpr int kAsmWaves = 4;
 
 // One wave per group: rows[g][i] = i where data packet i opened; the holes, ascending, take
-// the opened FEC packets, ascending (row k + j, plaintext copied into the slot); 255 where
-// none is left (the decode then reports the group as malformed, status -3).
+// the opened FEC packets, ascending (row k + j); 255 where none is left (the decode then
+// reports the group as malformed, status -3).  The open has already written each FEC packet
+// into the hole the length checks alone give it (fec_pre_slot); a pair the tag checks
+// changed is copied here.
 __global__ __launch_bounds__(kAsmWaves * 64) void open_assemble_kernel(
     int k, int m, int bb, long long groups, const uint8_t* __restrict__ pkt, long long pkt_stride,
-    const int32_t* __restrict__ ad_len, int ad_all, const int32_t* __restrict__ open_len,
-    uint8_t* blocks, uint8_t* rows) {
+    const int32_t* __restrict__ pkt_len, const int32_t* __restrict__ ad_len, int ad_all,
+    const int32_t* __restrict__ open_len, uint8_t* blocks, uint8_t* rows) {
     __shared__ uint8_t lavail[kAsmWaves][256], lhole[kAsmWaves][256];
+    __shared__ uint8_t prank[kAsmWaves][256], phole[kAsmWaves][256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long long g = (long long)blockIdx.x * kAsmWaves + w;
     if (g >= groups) return;   // uniform over the wave; no workgroup barrier below
@@ -685,11 +741,30 @@ __global__ __launch_bounds__(kAsmWaves * 64) void open_assemble_kernel(
         }
         nh += __popcll(bal);
     }
+    // the match the open wrote by (fec_pre_slot): ranks of the FEC packets and the holes by
+    // the length checks alone
+    int npa = 0, nph = 0;
+    for (int b0 = 0; b0 < m; b0 += 64) {
+        const int j = b0 + lane;
+        const bool v = j < m && open_len_ok(pkt_len, ad_len, ad_all, g * per + k + j, bb, pkt_stride);
+        const unsigned long long bal = __ballot(v);
+        if (j < m) prank[w][j] = v ? (uint8_t)(npa + __popcll(bal & below)) : (uint8_t)255;
+        npa += __popcll(bal);
+    }
+    for (int b0 = 0; b0 < k; b0 += 64) {
+        const int i = b0 + lane;
+        const bool miss = i < k && !open_len_ok(pkt_len, ad_len, ad_all, g * per + i, bb, pkt_stride);
+        const unsigned long long bal = __ballot(miss);
+        if (miss) phole[w][nph + __popcll(bal & below)] = (uint8_t)i;
+        nph += __popcll(bal);
+    }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     const int nfill = min(nh, na);
     for (int h = 0; h < nfill; ++h) {
         const int j = lavail[w][h], i = lhole[w][h];
+        const int pr = prank[w][j];
+        if (pr < nph && phole[w][pr] == i) continue;   // written there by the open
         const long long p = g * per + k + j;
         const uint8_t* src = pkt + p * pkt_stride + len_of(ad_len, ad_all, p) + 12;
         wave_copy_pad(blocks + (g * k + i) * (long long)bb, src, ol[k + j], bb, lane);
@@ -800,7 +875,7 @@ hipError_t launch_open_groups(int k, int m, int bb, long long groups,
     QPP_GO(open_group_kernel, dim3(tile_grid(n)), dim3(64), kTileBytes, st, k, m, bb, n, pkt,
            pkt_stride, pkt_len, ad_len, ad_all, blocks, open_len);
     qlaunch(open_assemble_kernel, dim3((unsigned)wg), dim3(kAsmWaves * 64), 0, st, k, m, bb,
-            groups, pkt, pkt_stride, ad_len, ad_all, open_len, blocks, rows);
+            groups, pkt, pkt_stride, pkt_len, ad_len, ad_all, open_len, blocks, rows);
     return hipGetLastError();
 }
 hipError_t launch_open_status(int k, int rmax, long long groups, const uint8_t* rows,
