@@ -525,7 +525,11 @@ def main():
         local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # QFEC_BENCH_PG=1 (under torchrun) keeps the process group at WORLD_SIZE = 1 too, so the
+    # N > 1 control flow (RCCL init, barriers, gathers, the max-over-ranks all_reduce) runs on
+    # one GPU: a rehearsal of the NCCL branch where no second GPU is available
+    pg = world > 1 or os.environ.get("QFEC_BENCH_PG") == "1"
+    if pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -644,14 +648,14 @@ def main():
 
     # ---- timed region: barrier + sync on both sides, K steps, nothing else on the stream
     # (no timing events: they cost A about 3 % of its step time)
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         timed_step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
@@ -670,7 +674,7 @@ def main():
         g_idx = torch.arange(G, device=dev)[:, None].expand(G, k)[slot]
         verified = verified and bool(torch.equal(out[slot], data[g_idx, rows_out.long()[slot]]))
     del g_idx
-    if world > 1:
+    if pg:
         flags = [None] * world
         dist.all_gather_object(flags, verified)
         verified = all(flags)
@@ -739,7 +743,7 @@ def main():
             "GiBps": round(G * k * payload / 2**30 / (elapsed / args.steps), 3),
             "encode_ms": round(enc_ms, 5), "decode_ms": round(dec_ms, 5),
             "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4)}
-    if world > 1:
+    if pg:
         per_rank = [None] * world
         dist.all_gather_object(per_rank, mine)
     else:
@@ -800,6 +804,7 @@ def main():
                 "k": k, "m": m, "payload_bytes": payload, "block_bytes": bb,
                 "losses_per_group": r,
                 "parallelism": f"{world} independent group shards (no collective)",
+                "process_group": f"{backend}, world {world}" if pg else "none",
                 "decode_layout": args.decode_layout, "loss_mode": args.loss_mode,
                 "parity_rows": args.parity,
                 "options": args.opt,
@@ -842,7 +847,7 @@ def main():
         print(json.dumps(line), flush=True)
 
     eng.close()
-    if world > 1:
+    if pg:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -48,7 +48,7 @@ def max_over_ranks(value, device=None):
     Used for the bench's elapsed time: the job is done when the slowest rank is."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64,
                      device=device if device is not None else "cpu")

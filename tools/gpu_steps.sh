@@ -7,6 +7,8 @@
 #   tests:<file|-k expr>  one test file (tests/test_gpu_pp.py) or a -k selection
 #   testlib:<name>,<file> one test file against quic_amd/libquic_fec_<name>.so
 #   mb:<name>             the microbenchmark binary tools/microbench/<name>
+#   pg1:<W>[:<args>]      bench.py under torchrun with one rank and the RCCL process group kept
+#                         (QFEC_BENCH_PG=1): the N > 1 control flow on one GPU
 #   smoke                 __graft_entry__.smoke()
 #   default               python bench.py (the driver's round-end line)
 #   bench:<W>[:<args>]    bench.py --workload W --verify (W = A B C D), extra args after ':'
@@ -44,6 +46,7 @@ for step in "$@"; do
     testlib) L="${W%%,*}"; F="${W#*,}"
             specs+=("$tag::900::QFEC_LIB_PATH=quic_amd/libquic_fec_$L.so python -u -m pytest $F -m gpu -x -q --timeout 120 --timeout-method thread") ;;
     mb)     specs+=("$tag::120::tools/microbench/$W") ;;
+    pg1)    specs+=("$tag::300::QFEC_BENCH_PG=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --workload $W --no-host --steps 10 --warmup 3 $extra") ;;
     default) specs+=("default::600::python bench.py") ;;
     smoke)  specs+=("smoke::300::python -c 'import __graft_entry__ as g; g.smoke()'") ;;
     bench)  specs+=("$tag::600::python bench.py --workload $W --verify $extra") ;;
