@@ -722,6 +722,9 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"enc_rc", &t.enc_rc, 2, 8},           {"prep_lane", &t.prep_lane, 0, 1},
         {"host_chunk_mb", &t.host_chunk_mb, 1, 4096},
         {"host_min_groups", &t.host_min_groups, 1, 1 << 20},
+        {"ring_wg", &t.ring_wg, -1, 1 << 20}, {"bsyn_wg", &t.bsyn_wg, -1, 1 << 20},
+        {"psyn_wg", &t.psyn_wg, 0, 1 << 20},  {"dcol_wg", &t.dcol_wg, 0, 1 << 20},
+        {"xor_wg", &t.xor_wg, 0, 1 << 20},
     };
     for (const Opt& o : opts) {
         if (strcmp(o.n, name) != 0) continue;
@@ -747,6 +750,8 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"psyn", t.psyn},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb}, {"host_min_groups", t.host_min_groups},
+        {"ring_wg", t.ring_wg}, {"bsyn_wg", t.bsyn_wg}, {"psyn_wg", t.psyn_wg},
+        {"dcol_wg", t.dcol_wg}, {"xor_wg", t.xor_wg},
     };
     for (const auto& o : opts)
         if (strcmp(o.first, name) == 0) { *value = o.second; return 0; }

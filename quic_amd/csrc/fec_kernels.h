@@ -42,6 +42,15 @@ struct Tune {
                               //   rows; 0: gf_apply)
     int dcol_grid = 0;        // gf_dcol: grid cap in workgroups (0: CUs x per-CU fit)
     int dcol_depth = 6;       // gf_dcol: blocks in flight per wave (6 or 8; two waves per SIMD)
+    // Oversubscribed grids: about this many groups (units) per wave, more workgroups than the
+    // device holds at once, so the hardware hands the last ones to whichever CU frees first
+    // (0: the resident persistent grid, every wave walking groups g0, g0 + W, ...; -1: the
+    // measured choice)
+    int ring_wg = -1;         // gf_ring encodes (-1: 1 for (32,4), (10,10), (5,5), (250,5))
+    int bsyn_wg = -1;         // gf_bsyn decode (-1: 2)
+    int psyn_wg = 0;          // gf_psyn decodes
+    int dcol_wg = 0;          // gf_dcol encode / decode (units = column tiles)
+    int xor_wg = 0;           // xor_dma (m = 1)
     int host_chunk_mb = 64;   // host-pointer batches: chunk size
     int host_min_groups = 512;  // host-pointer batches: at least this many groups per chunk
                                 //   (capped at 2 GiB of staging per buffer)

@@ -554,6 +554,10 @@ hipError_t launch_gf_bsyn(const uint8_t* in, uint8_t* out, const uint8_t* tab,
     const int per_cu = std::max(1, std::min((int)((160 * 1024) / lds), 20 / kBsynWaves));
     const long long want = (groups + kBsynWaves - 1) / kBsynWaves;
     long long cap = (long long)t.cus * per_cu;
+    // oversubscribed: about bwg groups per wave (B decode 0.60-0.61 -> 0.53-0.60 ms, DESIGN.md
+    // section 4.5)
+    const int bwg = t.bsyn_wg >= 0 ? t.bsyn_wg : 2;
+    if (bwg > 0) cap = (groups + (long long)kBsynWaves * bwg - 1) / ((long long)kBsynWaves * bwg);
     if (t.stream_grid > 0) cap = t.stream_grid;          // tests: many groups per wave
     const unsigned grid = (unsigned)std::min<long long>(want, cap);
     if ((groups + (long long)grid * kBsynWaves - 1) / ((long long)grid * kBsynWaves) * k >=

@@ -16,6 +16,8 @@ static unsigned dcol_grid(long long groups, const Tune& t, size_t lds, int wg_cu
     const long long want = (units + kDcWaves - 1) / kDcWaves;
     const int per_cu = std::max(1, std::min(wg_cu, (int)((160 * 1024) / lds)));
     long long cap = (long long)t.cus * per_cu;
+    if (t.dcol_wg > 0)   // oversubscribed: about dcol_wg units per wave
+        cap = (units + (long long)kDcWaves * t.dcol_wg - 1) / ((long long)kDcWaves * t.dcol_wg);
     if (t.dcol_grid > 0) cap = t.dcol_grid;          // tests: many units per wave
     return (unsigned)std::min<long long>(want, cap);
 }

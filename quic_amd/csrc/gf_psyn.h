@@ -417,6 +417,9 @@ hipError_t psyn_go_55(const PsynLaunch& a);
                                  : gf_psyn_kernel<KV, MV, RCV, kPsynS, 5, false>;             \
         const long long want = (a.groups + kPsynWaves - 1) / kPsynWaves;                       \
         long long cap = (long long)t.cus * resident_blocks((const void*)kern, kPsynWaves * 64, a.lds); \
+        if (t.psyn_wg > 0) /* oversubscribed: about psyn_wg groups per wave */                \
+            cap = (a.groups + (long long)kPsynWaves * t.psyn_wg - 1) /                         \
+                  ((long long)kPsynWaves * t.psyn_wg);                                         \
         if (t.stream_grid > 0) cap = t.stream_grid; /* tests: many groups per wave */          \
         const unsigned grid = (unsigned)std::min<long long>(want, cap);                       \
         if ((a.groups + (long long)grid * kPsynWaves - 1) / ((long long)grid * kPsynWaves) *   \

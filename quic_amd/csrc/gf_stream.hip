@@ -976,6 +976,15 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
         const size_t rlds = (size_t)kRingWaves * (RingShape<169>::RB + (rwide ? kStreamStage : 0));
         const long long rwant = (groups * (rsplit ? 2 : 1) + kRingWaves - 1) / kRingWaves;
         long long rcap = (long long)t.cus * (int)((160 * 1024) / rlds);
+        // oversubscribed: about rwg units per wave; measured faster for these encodes
+        // (B 0.58 -> 0.55 ms, (10,10) 0.361 -> 0.330; (10,20) and (15,15) no better,
+        // DESIGN.md section 4.5)
+        const int rwg = t.ring_wg >= 0 ? t.ring_wg
+                        : ((k == 32 && m == 4) || (k == 10 && m == 10) || (k == 5 && m == 5) ||
+                           (k == 250 && m == 5)) ? 1 : 0;
+        if (rwg > 0)
+            rcap = (groups * (rsplit ? 2 : 1) + (long long)kRingWaves * rwg - 1) /
+                   ((long long)kRingWaves * rwg);
         if (t.stream_grid > 0) rcap = t.stream_grid;
         const unsigned rgrid = (unsigned)std::min<long long>(rwant, rcap);
         if ((groups * (rsplit ? 2 : 1) + (long long)rgrid * kRingWaves - 1) / ((long long)rgrid * kRingWaves) >=

@@ -247,17 +247,23 @@ hipError_t launch_xor_dma(const uint8_t* in, uint8_t* out, const uint8_t* eidx,
     if (groups <= 0) return hipSuccess;
     XorPlan p;
     if (!xor_plan(k, bb, t, &p)) return hipErrorInvalidValue;
+    // the grid cap: one workgroup per CU, or (xor_wg) about xor_wg groups per wave
+    const int cap = t.xor_wg > 0
+                        ? (int)std::min<long long>((groups + (long long)p.waves * t.xor_wg - 1) /
+                                                       ((long long)p.waves * t.xor_wg),
+                                                   0x7fffffffLL)
+                        : t.cus;
     if (!decode)
         return xor_dispatch<false, false>(p, in, out, eidx, rows_in, rows_out, status, k, bb,
-                                          groups, out_gstride, st, t.cus);
+                                          groups, out_gstride, st, cap);
     if (rows_in && compact)
         return xor_dispatch<true, true, true>(p, in, out, eidx, rows_in, rows_out, status, k,
-                                              bb, groups, out_gstride, st, t.cus);
+                                              bb, groups, out_gstride, st, cap);
     if (rows_in)
         return xor_dispatch<true, true>(p, in, out, eidx, rows_in, rows_out, status, k, bb,
-                                        groups, out_gstride, st, t.cus);
+                                        groups, out_gstride, st, cap);
     return xor_dispatch<true, false>(p, in, out, eidx, rows_in, rows_out, status, k, bb, groups,
-                                     out_gstride, st, t.cus);
+                                     out_gstride, st, cap);
 }
 
 }  // namespace qfec
