@@ -724,6 +724,7 @@ int qfec_ctx_set_option(qfec_ctx* c, const char* name, int value) {
         {"host_min_groups", &t.host_min_groups, 1, 1 << 20},
         {"ring_wg", &t.ring_wg, -1, 1 << 20}, {"bsyn_wg", &t.bsyn_wg, -1, 1 << 20},
         {"psyn_wg", &t.psyn_wg, 0, 1 << 20},  {"dcol_wg", &t.dcol_wg, 0, 1 << 20},
+        {"stream_wg", &t.stream_wg, -1, 1 << 20},
         {"xor_wg", &t.xor_wg, 0, 1 << 20},
     };
     for (const Opt& o : opts) {
@@ -750,7 +751,7 @@ int qfec_ctx_get_option(qfec_ctx* c, const char* name, int* value) {
         {"bsyn", t.bsyn}, {"bsyn_depth", t.bsyn_depth}, {"psyn", t.psyn},
         {"pd", t.pd}, {"flat", t.flat}, {"enc_rc", t.enc_rc}, {"prep_lane", t.prep_lane},
         {"host_chunk_mb", t.host_chunk_mb}, {"host_min_groups", t.host_min_groups},
-        {"ring_wg", t.ring_wg}, {"bsyn_wg", t.bsyn_wg}, {"psyn_wg", t.psyn_wg},
+        {"ring_wg", t.ring_wg}, {"bsyn_wg", t.bsyn_wg}, {"psyn_wg", t.psyn_wg}, {"stream_wg", t.stream_wg},
         {"dcol_wg", t.dcol_wg}, {"xor_wg", t.xor_wg},
     };
     for (const auto& o : opts)

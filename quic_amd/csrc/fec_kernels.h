@@ -49,6 +49,8 @@ struct Tune {
     int ring_wg = -1;         // gf_ring encodes (-1: 1 for (32,4), (10,10), (5,5), (250,5))
     int bsyn_wg = -1;         // gf_bsyn decode (-1: 2)
     int psyn_wg = 0;          // gf_psyn decodes
+    int stream_wg = -1;       // gf_stream (run-time coefficients: the (250, 5) decode, other shapes;
+                              //   -1: 1 for groups of at least 64 KiB, else 0)
     int dcol_wg = 0;          // gf_dcol encode / decode (units = column tiles)
     int xor_wg = 0;           // xor_dma (m = 1)
     int host_chunk_mb = 64;   // host-pointer batches: chunk size

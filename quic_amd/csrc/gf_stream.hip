@@ -914,6 +914,10 @@ hipError_t launch_gf_stream(const uint8_t* in, uint8_t* out, const uint8_t* coef
     const long long units = groups * nchunk;
     const long long want = (units + kStreamWaves - 1) / kStreamWaves;
     long long cap = (long long)t.cus * per_cu;
+    // oversubscribed: about swg units per wave ((250, 5) decode 5.02 -> 4.36 ms, DESIGN.md
+    // section 4.5); large groups only by default
+    const int swg = t.stream_wg >= 0 ? t.stream_wg : ((long long)k * bb >= 65536 ? 1 : 0);
+    if (swg > 0) cap = (units + (long long)kStreamWaves * swg - 1) / ((long long)kStreamWaves * swg);
     if (t.stream_grid > 0) cap = t.stream_grid;          // tests: many groups per wave
     const unsigned grid = (unsigned)std::min<long long>(want, cap);
     const unsigned threads = kStreamWaves * 64;
