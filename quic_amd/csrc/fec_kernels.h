@@ -51,7 +51,8 @@ struct Tune {
     int psyn_wg = 0;          // gf_psyn decodes
     int stream_wg = -1;       // gf_stream (run-time coefficients: the (250, 5) decode, other shapes;
                               //   -1: 1 for groups of at least 64 KiB, else 0)
-    int dcol_wg = 0;          // gf_dcol encode / decode (units = column tiles)
+    int dcol_wg = 4;          // gf_dcol encode / decode (units = column tiles; D 1909 -> 2000 GiB/s
+                              //   over three alternating pairs on a power-limited box)
     int xor_wg = 0;           // xor_dma (m = 1)
     int host_chunk_mb = 64;   // host-pointer batches: chunk size
     int host_min_groups = 512;  // host-pointer batches: at least this many groups per chunk

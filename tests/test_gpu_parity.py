@@ -462,7 +462,8 @@ OPTION_SETS = [
     {"stream_static": 0}, {"bsyn": 0}, {"bsyn_depth": 5}, {"bsyn_depth": 7}, {"ring_split": 0},
     {"dcol": 0}, {"dcol_depth": 8},
     {"psyn": 0},
-    {"ring_wg": 0, "bsyn_wg": 0}, {"ring_wg": 3, "bsyn_wg": 5, "psyn_wg": 2, "dcol_wg": 4, "xor_wg": 3},
+    {"ring_wg": 0, "bsyn_wg": 0, "dcol_wg": 0, "stream_wg": 0},
+    {"ring_wg": 3, "bsyn_wg": 5, "psyn_wg": 2, "dcol_wg": 1, "xor_wg": 3, "stream_wg": 2},
 ]
 
 
