@@ -94,8 +94,10 @@ QFEC_API void qfec_ctx_destroy(qfec_ctx *ctx);
  * (their wide parity stores), "dcol" 0/1, "dcol_grid" 0.., "dcol_depth" 6/8, "bsyn" 0/1,
  * "bsyn_depth" 3/5/7, "psyn" 0/1, "psyn_wide" 0..2 (wide recovered-block stores: none,
  * (10, 10), every code), "pd" 1..3, "flat" 0/1, "enc_rc" 2/4/8, "prep_lane" 0/1,
- * "host_chunk_mb" 1..4096, "host_min_groups" 1...  get also reads "cus" (compute units of the
- * device).  -2 for an unknown name or a value out of range (also for the measured-and-removed
+ * "host_chunk_mb" 1..4096, "host_min_groups" 1.., "ring_split" 0/1 ((10, 20) encode in two
+ * units), and the grid shares "ring_wg", "bsyn_wg", "stream_wg" (-1 = the measured choice),
+ * "psyn_wg", "dcol_wg", "xor_wg" (groups per wave of an oversubscribed grid; 0 = the resident
+ * persistent grid).  get also reads "cus" (compute units of the device).  -2 for an unknown name or a value out of range (also for the measured-and-removed
  * variants of earlier versions).  No environment variable changes what the library launches. */
 QFEC_API int qfec_ctx_set_option(qfec_ctx *ctx, const char *name, int value);
 QFEC_API int qfec_ctx_get_option(qfec_ctx *ctx, const char *name, int *value);
